@@ -1,0 +1,114 @@
+"""Loading helpers for the golden fixtures (tests/golden/*.safetensors). Test infrastructure only."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+from functools import lru_cache
+
+import torch
+from safetensors import safe_open
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, GOLDEN)
+import procedural as P  # noqa: E402
+
+CASES = ["tiny_vit_cls", "tiny_vit_patches", "tiny_clip336_patches", "tiny_clip336_cls", "cfg1_b2_patches"]
+
+
+@lru_cache(maxsize=None)
+def load(name: str):
+    path = os.path.join(GOLDEN, f"{name}.safetensors")
+    with safe_open(path, "pt") as f:
+        meta = json.loads(f.metadata()["meta"])
+        tensors = {k: f.get_tensor(k) for k in f.keys()}
+    return meta, tensors
+
+
+def enc_desc(meta) -> dict:
+    """Encoder geometry from the fixture's HF config kwargs (ViTConfig()/CLIPVisionConfig() defaults)."""
+    c = dict(meta["enc_cfg"])
+    if meta["enc_kind"] == "vit":
+        base = dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072,
+                    image_size=224, patch_size=16, eps=1e-12)
+    else:
+        base = dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072,
+                    image_size=224, patch_size=32, eps=1e-5)
+    base.update(c)
+    return {"kind": meta["enc_kind"], "hidden": base["hidden_size"], "layers": base["num_hidden_layers"],
+            "heads": base["num_attention_heads"], "mlp": base["intermediate_size"],
+            "image": base["image_size"], "patch": base["patch_size"], "eps": base["eps"]}
+
+
+def dec_desc(meta) -> dict:
+    d = meta["dec"]
+    return {"vocab": d["vocab"], "d": d["embed_dim"], "heads": d["heads"], "layers": d["layers"],
+            "ff": d["ff"], "max_seq_len": d.get("max_seq_len", 100)}
+
+
+def state(meta):
+    spec = [(n, tuple(s)) for n, s in meta["spec"]]
+    st = P.make_state(spec, meta["seed"])
+    chk = P.checksum(st[n] for n, _ in spec)
+    assert abs(chk - meta["weights_checksum"]) <= 1e-9 * max(1.0, abs(chk)), "procedural weights drifted"
+    return st
+
+
+def inputs(meta, step: int = 0):
+    imgs = P.make_images(meta["B"], meta["image_size"], meta["seed"] + 1)
+    cap = P.make_captions(meta["B"], meta["cap_len"], meta["dec"]["vocab"], meta["seed"] + 2 + step,
+                          meta["lengths"])
+    return imgs, cap[:, :-1].contiguous(), cap[:, 1:].contiguous()
+
+
+def trainable_names(meta):
+    return [n for n, _ in meta["spec"] if not n.startswith("encoder.")]
+
+
+def degenerate_mask(name: str, t: torch.Tensor, meta=None):
+    """Elements whose reference gradient is exactly 0 in real arithmetic (so the stored value is
+    rounding noise, ~1e-10, that AdamW then normalises to an arbitrary +-lr step): the KEY part of a
+    packed in_proj_bias — softmax is invariant to a per-row constant, so d(loss)/d(b_k) = 0.
+    Returns a bool mask of the elements that ARE pinned, or None."""
+    cls_cross = meta is not None and meta.get("mode") == "cls" and "multihead_attn" in name
+    if name.endswith("in_proj_bias"):
+        d = t.numel() // 3
+        m = torch.ones(t.numel(), dtype=torch.bool)
+        m[(0 if cls_cross else d):2 * d] = False
+        return m
+    # cls mode: memory length S = 1 and softmax over one key == 1, so the cross-attention QUERY and
+    # KEY projections get exactly-zero gradients as well
+    if cls_cross and name.endswith("in_proj_weight"):
+        n = t.numel()
+        d = int(round((n / 3) ** 0.5))
+        m = torch.ones(n, dtype=torch.bool)
+        m[:2 * d * d] = False
+        return m
+    return None
+
+
+def compare_stat(prefix, name, t, tensors, meta, rtol, atol):
+    """Compare a tensor to its fixture entry (full / sample+stats). Returns max abs err on samples."""
+    t = t.detach().float().cpu()
+    if f"{prefix}.full.{name}" in tensors:
+        ref = tensors[f"{prefix}.full.{name}"]
+        got = t.reshape(ref.shape)
+        m = degenerate_mask(name, ref, meta) if prefix.startswith("delta") else None
+        if m is not None:
+            got, ref = got.flatten()[m], ref.flatten()[m]
+            # the unpinned elements still obey |delta| <= lr-ish bound (checked by the caller's bound)
+        torch.testing.assert_close(got, ref, rtol=rtol, atol=atol, msg=lambda s: f"{prefix} {name}: {s}")
+        return float((got - ref).abs().max())
+    idx = torch.tensor(meta["sample_index"][name])
+    ref = tensors[f"{prefix}.sample.{name}"]
+    got = t.flatten()[idx]
+    m = degenerate_mask(name, t.flatten(), meta) if prefix.startswith("delta") else None
+    if m is not None:
+        got, ref = got[m[idx]], ref[m[idx]]
+    torch.testing.assert_close(got, ref, rtol=rtol, atol=atol, msg=lambda s: f"{prefix} {name}: {s}")
+    st = tensors[f"{prefix}.stats.{name}"].double()
+    flat = t.flatten().double()
+    norm = flat.norm()
+    if m is None:
+        assert abs(norm - st[1]) <= rtol * abs(st[1]) + atol * flat.numel() ** 0.5, f"{prefix} {name} norm"
+    return float((got - ref).abs().max())
