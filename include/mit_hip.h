@@ -1,0 +1,206 @@
+/* mit_hip.h — C ABI of libmit_hip.so, the MI355X (gfx950) kernels behind the captioning train step
+ * of wazzuck/multimodal-image-transformer (frozen ViT/CLIP encoder + Transformer decoder).
+ *
+ * The reference has no native FFI: its "operator API" is the torch.nn / HF modules it calls
+ * (SURVEY.md §8b). Each entry point below names the reference call site (file:line under
+ * /root/reference, or the torch/transformers code those lines dispatch to) that it replaces.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers + element counts/strides; no torch types. `stream` is a hipStream_t
+ *     (NULL = default stream). Every launch is asynchronous on that stream; no entry point
+ *     allocates, frees or synchronises, so any sequence of calls can be captured into a hipGraph.
+ *   - dtype: MIT_BF16 (bf16 storage, fp32 math) or MIT_F32 (fp32 end to end: parity mode).
+ *     Master weights, gradients, optimizer state, LayerNorm statistics and losses are always f32.
+ *   - return 0 on success; MIT_ERR_INVALID for a rejected argument (nothing launched),
+ *     MIT_ERR_HIP for a launch failure; mit_last_error() returns the message (thread-local).
+ *   - dropout: p in [0,1); keep(i) = hash(*seed, site, i) >= p*2^32, kept values scaled by
+ *     1/(1-p). `seed` is a DEVICE pointer (so graph replays draw fresh masks); NULL means 0.
+ */
+#ifndef MIT_HIP_H
+#define MIT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIT_OK 0
+#define MIT_ERR_INVALID 1
+#define MIT_ERR_HIP 2
+
+enum { MIT_F32 = 0, MIT_BF16 = 1 };
+enum { MIT_K_CONTIG = 0, MIT_MN_CONTIG = 1 };
+enum { MIT_ACT_NONE = 0, MIT_ACT_RELU = 1, MIT_ACT_GELU = 2, MIT_ACT_QUICK_GELU = 3 };
+
+const char* mit_last_error(void);
+int mit_abi_version(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * GEMM with fused epilogue. Replaces every nn.Linear / F.linear / addmm / mm of the hot path:
+ *   encoder  tf/models/vit/modeling_vit.py:213-215,233,249-254 (q/k/v, o_proj, fc1+GELU, fc2+res)
+ *            tf/models/clip/modeling_clip.py:338-350 (fc1 + quick_gelu)
+ *   model    model.py:99,145 (projection)
+ *   decoder  torch/nn/functional.py:6435 (packed in_proj), torch/nn/modules/transformer.py:1197-1199
+ *            (linear1 + ReLU + dropout, linear2), decoder.py:124,191 (fc_out)
+ *   backward the dX / dW products autograd would issue for the same layers (train.py:93).
+ *
+ * C[m,n] = out( dropout( auxmask( act( alpha * sum_k A(m,k) B(k,n) + bias[n] ) ) ) + residual[m,n] )
+ *   A(m,k) = A[m*lda+k] (a_layout K_CONTIG) or A[k*lda+m] (MN_CONTIG)
+ *   B(k,n) = B[n*ldb+k] (b_layout K_CONTIG) or B[k*ldb+n] (MN_CONTIG)
+ *   auxmask: if aux != NULL, multiply by (aux[m*ld_aux+n] > 0 ? aux_scale : 0)  (ReLU/dropout bwd)
+ *   dropout index = m*N + n ; residual/aux in the operand dtype; bias f32 [N]
+ *   out_f32: write f32 (accumulate: C += value), else the operand dtype.
+ * bf16 requirements: lda, ldb and the contiguous extent of each operand multiples of 8; A, B 16-B aligned. */
+typedef struct {
+  int dtype, a_layout, b_layout;
+  long M, N, K;
+  const void* A;
+  long lda;
+  const void* B;
+  long ldb;
+  void* C;
+  long ldc;
+  float alpha;
+  const float* bias;
+  int act;
+  const void* residual;
+  long ldr;
+  const void* aux;
+  long ld_aux;
+  float aux_scale;
+  float drop_p;
+  const uint64_t* seed;
+  uint32_t site;
+  int out_f32;
+  int accumulate;
+} mit_gemm_args;
+int mit_gemm(const mit_gemm_args* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * LayerNorm over the last dim, fp32 statistics.
+ * Replaces nn.LayerNorm in tf/models/vit/modeling_vit.py:274,281,385 (pre-LN, eps 1e-12),
+ * tf/models/clip/modeling_clip.py:358,360,642 (eps 1e-5) and the post-LN residual blocks of
+ * torch/nn/modules/transformer.py:1144-1153: y = LN(x + dropout(r)).
+ *   r may be NULL (plain LN). z (may be NULL) receives x + dropout(r) (saved for the backward).
+ *   mean/rstd (f32 [rows], may be NULL) saved for the backward. gamma/beta f32 [cols]. */
+int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x, long ldx, const void* r, long ldr,
+                      float r_drop_p, const uint64_t* seed, uint32_t site, const float* gamma, const float* beta,
+                      float eps, void* z, void* y, long ldy, float* mean, float* rstd, void* stream);
+
+/* Backward of y = LN(z), z = x + dropout(r):
+ *   dz = dLN(dy) (+ dy_extra if not NULL, an extra gradient arriving at z... unused: pass NULL)
+ *   dx = dz (written to dx, may alias dy), dr = dz * dropout_mask (may be NULL)
+ *   dgamma/dbeta: f32 [cols], ACCUMULATED (+=) — the caller zeroes them once per step.
+ *   ws: f32 workspace of >= mit_layernorm_bwd_ws_floats(rows, cols) floats. */
+long mit_layernorm_bwd_ws_floats(long rows, long cols);
+int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy, const void* z, const float* mean,
+                      const float* rstd, const float* gamma, void* dx, void* dr, float r_drop_p, const uint64_t* seed,
+                      uint32_t site, float* dgamma, float* dbeta, float* ws, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Scaled-dot-product attention, head_dim 64, heads interleaved inside a token row (column h*64).
+ * Replaces: encoder MHSA (tf/models/vit/modeling_vit.py:164-189, no mask, scale 1/8);
+ * decoder self-attention with the merged causal + key-padding float mask and attention dropout
+ * (torch/nn/functional.py:6370-6404, 6553-6566, 6615-6633; masks from utils.py:30-36,66 — the
+ * mask is never materialised: key j of batch b is masked iff j > i (causal) or
+ * key_tokens[b*tok_batch + j] == pad_idx); decoder cross-attention (no mask).
+ * Element strides: X(b, t, h, :) = X + b*X_batch + t*X_row + h*64. lse: f32 [B*H*Lq] (log-sum-exp
+ * of the scaled, masked scores; required by the backward). A fully masked row yields NaN, as in
+ * the reference. */
+typedef struct {
+  const void* q;
+  long q_row, q_batch;
+  const void* k;
+  long k_row, k_batch;
+  const void* v;
+  long v_row, v_batch;
+  void* o;
+  long o_row, o_batch;
+  float* lse;
+  const int64_t* key_tokens;
+  long tok_batch;
+  int pad_idx;
+  int causal;
+  float scale;
+  float drop_p;
+  const uint64_t* seed;
+  uint32_t site;
+} mit_attn_args;
+int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, long Dh, const mit_attn_args* a, void* stream);
+
+/* Backward (autograd of the same SDPA call). dq/dk/dv are overwritten (not accumulated).
+ * delta_ws: f32 [B*H*Lq] workspace. */
+typedef struct {
+  const void* dout;
+  long do_row, do_batch;
+  void* dq;
+  long dq_row, dq_batch;
+  void* dk;
+  long dk_row, dk_batch;
+  void* dv;
+  long dv_row, dv_batch;
+  float* delta_ws;
+} mit_attn_grads;
+int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, long Dh, const mit_attn_args* a,
+                      const mit_attn_grads* g, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Encoder input assembly.
+ * im2col of the patch Conv2d (tf/models/vit/modeling_vit.py:60,69; clip 148-154):
+ *   out[(b*np + p) * kpad + (c*P*P + ky*P + kx)] = img[b, c, py*P+ky, px*P+kx]; columns >= C*P*P are 0.
+ * assemble (modeling_vit.py:146-157, modeling_clip.py:212-219):
+ *   h[b, 0, :] = cls + pos[0];  h[b, 1+p, :] = patch[b*np+p] + pos[1+p]. */
+int mit_im2col(int dtype, long B, long C, long H, long W, long P, const float* img, void* out, long kpad, void* stream);
+int mit_vit_assemble(int dtype, long B, long np, long E, const void* patch, const float* cls, const float* pos, void* h,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Decoder input: x = dropout(Emb[tok] * scale + pe[t]) (decoder.py:168-171, 71-72).
+ * table in the operand dtype [V, d]; pe f32 [>=T, d]. */
+int mit_embed_fwd(int dtype, long B, long T, long d, const int64_t* tokens, const void* table, float scale,
+                  const float* pe, float drop_p, const uint64_t* seed, uint32_t site, void* out, void* stream);
+/* dtable[tok] += scale * dropout_mask * dx (f32, atomics; caller zeroes dtable); the padding_idx
+ * row receives no gradient (nn.Embedding(padding_idx=PAD), decoder.py:105). */
+int mit_embed_bwd(int dtype, long B, long T, long d, const int64_t* tokens, const void* dx, float scale, float drop_p,
+                  const uint64_t* seed, uint32_t site, int pad_idx, float* dtable, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Cross-entropy with ignore_index (train.py:90,327 -> torch/nn/functional.py cross_entropy).
+ * count_targets: *count += #(targets != ignore) as f32 (device scalar, caller zeroes).
+ * ce: per row of logits [rows, V] (ld): loss_sum += -log_softmax(row)[t] for t != ignore;
+ *     if want_grad, logits are overwritten IN PLACE by d(loss)/d(logits) =
+ *     (softmax - onehot) * grad_scale[0], and by 0 for ignored rows. grad_scale is a device scalar
+ *     (1 / global non-PAD count: the reference's mean reduction, exact under data parallelism). */
+int mit_count_targets(const int64_t* targets, long n, int ignore_index, float* count, void* stream);
+int mit_cross_entropy(int dtype, long rows, long V, void* logits, long ld, const int64_t* targets, int ignore_index,
+                      const float* grad_scale, float* loss_sum, int want_grad, void* stream);
+
+/* bias gradient: out[n] (+)= sum_m dy[m*ld + n]  (f32 out; accumulate flag) */
+int mit_colsum(int dtype, long M, long N, const void* dy, long ld, float* out, int accumulate, float* ws, void* stream);
+long mit_colsum_ws_floats(long M, long N);
+
+/* ---------------------------------------------------------------------------------------------
+ * Optimizer: torch.nn.utils.clip_grad_norm_ (train.py:96-97; torch/nn/utils/clip_grad.py:165-186)
+ * fused with torch.optim.AdamW (train.py:100,319-325; torch/optim/adam.py:419-547) over ONE flat
+ * f32 parameter buffer. Sequence per step: mit_grad_norm (total norm + clip coefficient into
+ * `norm_out` = {total_norm, coef}) then mit_adamw (reads coef, lr and the step count from device
+ * memory, increments nothing — mit_step_inc bumps the device step counter first). */
+long mit_grad_norm_ws_floats(long n);
+int mit_grad_norm(const float* grads, long n, float max_norm, float* ws, float* norm_out, void* stream);
+int mit_step_inc(int64_t* step, void* stream);
+int mit_adamw(long n, float* param, const float* grad, float* m, float* v, void* shadow_bf16, const float* norm_out,
+              const float* lr, const int64_t* step, float beta1, float beta2, float eps, float weight_decay,
+              void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Utilities. cast: f32 -> operand dtype copy (weights to the bf16 shadow); fill f32.
+ * dropout_mask_debug: writes the keep-multiplier (0 or 1/(1-p)) the kernels use at
+ * (seed, site, idx) for idx in [0, n) — tests rebuild reference masks from it. */
+int mit_cast_f32(int dtype, long n, const float* src, void* dst, void* stream);
+int mit_dropout_mask(long n, float p, const uint64_t* seed, uint32_t site, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

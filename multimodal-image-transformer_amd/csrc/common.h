@@ -1,0 +1,107 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels of the captioning train step.
+// Wave64 everywhere; bf16 activations with fp32 accumulation, or fp32 end to end (parity mode).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mit_hip.h"
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// ---------------------------------------------------------------------------------------------
+// Counter-based dropout RNG: keep(i) = mix64(seed ^ site, i) >= p * 2^32. Stateless, so the
+// backward regenerates the forward's mask from (seed, site, element index) without storing it.
+// The seed lives in device memory so a captured hipGraph replays with a fresh seed per step.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix_u32(uint64_t key, uint64_t idx) {
+  uint64_t x = key ^ (idx * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 31;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 29;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 32;
+  return (uint32_t)x;
+}
+__device__ __forceinline__ uint64_t site_key(const uint64_t* seed, uint32_t site) {
+  return (seed ? *seed : 0ull) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(site + 1));
+}
+// returns the dropout multiplier (0 or 1/(1-p)) for element idx
+__device__ __forceinline__ float drop_mul(uint64_t key, uint64_t idx, uint32_t thresh, float scale) {
+  return mix_u32(key, idx) >= thresh ? scale : 0.0f;
+}
+static inline uint32_t drop_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  if (t >= 4294967295.0) t = 4294967295.0;
+  return (uint32_t)t;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave64 reductions
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block reduction (blockDim multiple of 64, <= 1024); scratch >= 16 floats
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float r = (l < nw) ? scratch[l] : 0.0f;
+  r = wave_sum(r);
+  return r;
+}
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float r = (l < nw) ? scratch[l] : -INFINITY;
+  r = wave_max(r);
+  return r;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+
+// error plumbing shared by every C-ABI entry point (capi.cpp)
+int mit_set_error(const char* fmt, ...);
+#define MIT_CHECK_ARG(cond, ...)          \
+  do {                                    \
+    if (!(cond)) {                        \
+      mit_set_error(__VA_ARGS__);         \
+      return MIT_ERR_INVALID;             \
+    }                                     \
+  } while (0)
+#define MIT_LAUNCH_CHECK(name)                                              \
+  do {                                                                      \
+    hipError_t e_ = hipGetLastError();                                      \
+    if (e_ != hipSuccess) {                                                 \
+      mit_set_error("%s: launch failed: %s", name, hipGetErrorString(e_));  \
+      return MIT_ERR_HIP;                                                   \
+    }                                                                       \
+  } while (0)

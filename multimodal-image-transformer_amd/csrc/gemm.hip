@@ -1,0 +1,335 @@
+// Dense GEMM for every contraction of the train step (SURVEY.md §2b rows E1,E4,E6,E7,P1,D3,D5-D8
+// and their backward): C[M,N] = epi( alpha * sum_k A(m,k) * B(k,n) ).
+//
+// Operand storage (no transpose copies ever):
+//   A: MIT_K_CONTIG  -> A[m*lda + k]      (activations X, dY)
+//      MIT_MN_CONTIG -> A[k*lda + m]      (dY^T in weight-grad GEMMs)
+//   B: MIT_K_CONTIG  -> B[n*ldb + k]      (nn.Linear weight W[out,in] in Y = X W^T)
+//      MIT_MN_CONTIG -> B[k*ldb + n]      (W in dX = dY W, X in dW = dY^T X)
+//
+// bf16 path: 128x128x64 block tile, 4 waves (2x2), each wave 64x64 = 4x4 tiles of
+// v_mfma_f32_16x16x32_bf16, fp32 accumulation. Global -> registers -> LDS double buffer (one
+// barrier per K step). K-contig tiles are XOR-swizzled for conflict-free ds_read_b128 fragment
+// reads; MN-contig tiles are read with ds_read_b64_tr_b16 (CDNA4 hardware transpose) so the same
+// kernel serves NT / NN / TN without materialising a transpose.
+// fp32 path (parity mode): a plain LDS-tiled FMA kernel with the identical epilogue.
+#include "common.h"
+
+namespace {
+
+struct Epi {
+  const float* bias;
+  const void* res;
+  long ldr;
+  const void* aux;
+  long ld_aux;
+  float aux_scale;
+  float alpha;
+  int act;
+  int out_f32;
+  int accumulate;
+  const uint64_t* seed;
+  uint32_t site;
+  uint32_t thresh;
+  float dscale;
+  int dropout;
+};
+
+template <typename T>
+__device__ __forceinline__ void epi_store(const Epi& e, void* C, long ldc, long N, long r, long c, float v) {
+  v *= e.alpha;
+  if (e.bias) v += e.bias[c];
+  if (e.act == MIT_ACT_RELU) v = fmaxf(v, 0.0f);
+  else if (e.act == MIT_ACT_GELU) v = gelu_erf(v);
+  else if (e.act == MIT_ACT_QUICK_GELU) v = quick_gelu(v);
+  if (e.aux) v *= (to_f(((const T*)e.aux)[r * e.ld_aux + c]) > 0.0f) ? e.aux_scale : 0.0f;
+  if (e.dropout) v *= drop_mul(site_key(e.seed, e.site), (uint64_t)r * (uint64_t)N + (uint64_t)c, e.thresh, e.dscale);
+  if (e.res) v += to_f(((const T*)e.res)[r * e.ldr + c]);
+  if (e.out_f32) {
+    float* o = (float*)C + r * ldc + c;
+    if (e.accumulate) v += *o;
+    *o = v;
+  } else {
+    ((T*)C)[r * ldc + c] = from_f<T>(v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// bf16 MFMA kernel
+// ------------------------------------------------------------------------------------------------
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand per stage
+
+// byte offset of 16-B chunk c (0..7) of row r in a K-contig [128][64] bf16 tile
+__device__ __forceinline__ int koff(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+// swizzle of a k-row in an MN-contig [64][128] bf16 tile (256-B rows); see header comment
+__device__ __forceinline__ int mn_swz(int kr) { return ((kr & 3) | ((((kr >> 2) ^ (kr >> 3)) & 1) << 2)) << 5; }
+__device__ __forceinline__ int mnoff(int kr, int byte_in_row) { return kr * 256 + (byte_in_row ^ mn_swz(kr)); }
+
+template <int LAY>
+struct Stage {
+  u32x4 r[4];
+  // load a BM(or BN) x BK tile starting at (row0 = m/n offset, k0) into registers
+  __device__ __forceinline__ void load(const bf16* __restrict__ g, long ld, long rows_total, long K, long row0, long k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i;
+      bool ok;
+      long off;
+      if (LAY == MIT_K_CONTIG) {
+        const int r = id >> 3, c = id & 7;
+        ok = (row0 + r < rows_total) && (k0 + c * 8 < K);
+        off = (row0 + r) * ld + k0 + c * 8;
+      } else {
+        const int kr = id >> 4, c = id & 15;
+        ok = (k0 + kr < K) && (row0 + c * 8 < rows_total);
+        off = (k0 + kr) * ld + row0 + c * 8;
+      }
+      if (ok) r[i] = *(const u32x4*)(g + off);
+      else r[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i;
+      int off;
+      if (LAY == MIT_K_CONTIG) off = koff(id >> 3, id & 7);
+      else off = mnoff(id >> 4, (id & 15) * 16);
+      *(u32x4*)(lds + off) = r[i];
+    }
+  }
+};
+
+// MFMA operand fragment: rows [rbase, rbase+16) of the tile, k-slice kk (32 wide)
+template <int LAY>
+__device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kk, int lane) {
+  if (LAY == MIT_K_CONTIG) {
+    const int r = rbase + (lane & 15), c = kk * 4 + (lane >> 4);
+    u32x4 v = *(const u32x4*)(lds + koff(r, c));
+    return __builtin_bit_cast(bf16x8, v);
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int k0 = kk * 32 + g * 8 + q;
+    const int colb = (rbase + 4 * p) * 2;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + mnoff(k0, colb)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, lds + mnoff(k0 + 4, colb)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <int ALAY, int BLAY>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
+                                                        long M, long N, long K, long lda, long ldb, long ldc, Epi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // XCD-aware tile order: consecutive hardware block ids round-robin over 8 XCDs; give each
+  // XCD a contiguous run of tiles so neighbours share A/B panels in its L2 (guide §5.5 T1).
+  const int nbn = (int)((N + BN - 1) / BN), nbm = (int)((M + BM - 1) / BM);
+  const int nwg = nbn * nbm;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg / 8, rr = nwg % 8, x = bid % 8, y = bid / 8;
+    bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + y;
+  }
+  // group tiles in column-panels of 8 M-blocks for L2 reuse of B
+  const int GROUP = 8;
+  const int group_id = bid / (GROUP * nbn);
+  const int first_m = group_id * GROUP;
+  const int gsize = min(nbm - first_m, GROUP);
+  const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
+  const int bn = (bid % (GROUP * nbn)) / gsize;
+  const long m0 = (long)bm * BM, n0 = (long)bn * BN;
+
+  // stage buffer b: A tile at smem + b*2*TILE_BYTES, B tile right after it
+#define AS(b) (smem + (b) * 2 * TILE_BYTES)
+#define BS(b) (smem + (b) * 2 * TILE_BYTES + TILE_BYTES)
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage<ALAY> sa;
+  Stage<BLAY> sb;
+  const int nk = (int)((K + BK - 1) / BK);
+  sa.load(A, lda, M, K, m0, 0, tid);
+  sb.load(B, ldb, N, K, n0, 0, tid);
+  sa.store(AS(0), tid);
+  sb.store(BS(0), tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      sa.load(A, lda, M, K, m0, (long)(kt + 1) * BK, tid);
+      sb.load(B, ldb, N, K, n0, (long)(kt + 1) * BK, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag<ALAY>(AS(cur), wm * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BLAY>(BS(cur), wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      sa.store(AS(cur ^ 1), tid);
+      sb.store(BS(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long c = n0 + wn * 64 + j * 16 + (lane & 15);
+      if (c >= N) continue;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const long r = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + t;
+        if (r < M) epi_store<bf16>(e, C, ldc, N, r, c, acc[i][j][t]);
+      }
+    }
+#undef AS
+#undef BS
+}
+
+// ------------------------------------------------------------------------------------------------
+// fp32 FMA kernel (parity mode): 64x64x16 tile, 256 threads x (4x4) outputs
+// ------------------------------------------------------------------------------------------------
+template <int ALAY, int BLAY>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, const float* __restrict__ B, void* C,
+                                                       long M, long N, long K, long lda, long ldb, long ldc, Epi e) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][64 + 4];
+  const int tid = threadIdx.x;
+  const long m0 = (long)blockIdx.y * 64, n0 = (long)blockIdx.x * 64;
+  const int tm = (tid >> 4) * 4, tn = (tid & 15) * 4;
+  float acc[4][4] = {};
+  for (long k0 = 0; k0 < K; k0 += 16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i;  // 0..1023 over 64 x 16
+      int mm, kk;
+      if (ALAY == MIT_K_CONTIG) { mm = id >> 4; kk = id & 15; } else { kk = id >> 6; mm = id & 63; }
+      const long gm = m0 + mm, gk = k0 + kk;
+      float v = 0.f;
+      if (gm < M && gk < K) v = (ALAY == MIT_K_CONTIG) ? A[gm * lda + gk] : A[gk * lda + gm];
+      As[kk][mm] = v;
+      int nn;
+      if (BLAY == MIT_K_CONTIG) { nn = id >> 4; kk = id & 15; } else { kk = id >> 6; nn = id & 63; }
+      const long gn = n0 + nn, gk2 = k0 + kk;
+      float w = 0.f;
+      if (gn < N && gk2 < K) w = (BLAY == MIT_K_CONTIG) ? B[gn * ldb + gk2] : B[gk2 * ldb + gn];
+      Bs[kk][nn] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][tm + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tn + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long r = m0 + tm + i, c = n0 + tn + j;
+      if (r < M && c < N) epi_store<float>(e, C, ldc, N, r, c, acc[i][j]);
+    }
+}
+
+template <int AL, int BL>
+void launch_bf16(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
+  const long nbm = (g->M + BM - 1) / BM, nbn = (g->N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), dim3((unsigned)(nbm * nbn)), dim3(256), 4 * TILE_BYTES, s,
+                     (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, e);
+}
+template <int AL, int BL>
+void launch_f32(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
+  dim3 grid((unsigned)((g->N + 63) / 64), (unsigned)((g->M + 63) / 64));
+  hipLaunchKernelGGL((gemm_f32_kernel<AL, BL>), grid, dim3(256), 0, s, (const float*)g->A, (const float*)g->B, g->C, g->M,
+                     g->N, g->K, g->lda, g->ldb, g->ldc, e);
+}
+
+}  // namespace
+
+static bool mit_gemm_smem_set = false;
+
+extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
+  MIT_CHECK_ARG(g != nullptr, "mit_gemm: null args");
+  MIT_CHECK_ARG(g->dtype == MIT_F32 || g->dtype == MIT_BF16, "mit_gemm: bad dtype %d", g->dtype);
+  MIT_CHECK_ARG(g->M >= 0 && g->N >= 0 && g->K >= 0, "mit_gemm: negative extent");
+  MIT_CHECK_ARG(g->A && g->B && g->C, "mit_gemm: null operand");
+  MIT_CHECK_ARG(g->a_layout == MIT_K_CONTIG || g->a_layout == MIT_MN_CONTIG, "mit_gemm: bad a_layout");
+  MIT_CHECK_ARG(g->b_layout == MIT_K_CONTIG || g->b_layout == MIT_MN_CONTIG, "mit_gemm: bad b_layout");
+  if (g->M == 0 || g->N == 0) return MIT_OK;
+  MIT_CHECK_ARG(g->lda >= (g->a_layout == MIT_K_CONTIG ? g->K : g->M), "mit_gemm: lda too small");
+  MIT_CHECK_ARG(g->ldb >= (g->b_layout == MIT_K_CONTIG ? g->K : g->N), "mit_gemm: ldb too small");
+  MIT_CHECK_ARG(g->ldc >= g->N, "mit_gemm: ldc too small");
+  MIT_CHECK_ARG(!g->accumulate || g->out_f32, "mit_gemm: accumulate needs an f32 output");
+  if (g->dtype == MIT_BF16) {
+    // 16-byte vector staging: contiguous extents and leading dims in multiples of 8 elements
+    MIT_CHECK_ARG(g->lda % 8 == 0 && g->ldb % 8 == 0, "mit_gemm(bf16): lda/ldb must be multiples of 8");
+    MIT_CHECK_ARG(g->a_layout == MIT_MN_CONTIG ? g->M % 8 == 0 : g->K % 8 == 0,
+                  "mit_gemm(bf16): A's contiguous extent must be a multiple of 8");
+    MIT_CHECK_ARG(g->b_layout == MIT_MN_CONTIG ? g->N % 8 == 0 : g->K % 8 == 0,
+                  "mit_gemm(bf16): B's contiguous extent must be a multiple of 8");
+    MIT_CHECK_ARG(((uintptr_t)g->A % 16) == 0 && ((uintptr_t)g->B % 16) == 0, "mit_gemm(bf16): A/B must be 16-B aligned");
+  }
+  Epi e;
+  e.bias = g->bias;
+  e.res = g->residual;
+  e.ldr = g->ldr;
+  e.aux = g->aux;
+  e.ld_aux = g->ld_aux;
+  e.aux_scale = g->aux_scale;
+  e.alpha = g->alpha;
+  e.act = g->act;
+  e.out_f32 = g->out_f32;
+  e.accumulate = g->accumulate;
+  e.seed = g->seed;
+  e.site = g->site;
+  e.dropout = g->drop_p > 0.0f;
+  e.thresh = drop_threshold(g->drop_p);
+  e.dscale = g->drop_p < 1.0f ? 1.0f / (1.0f - g->drop_p) : 0.0f;
+  hipStream_t s = (hipStream_t)stream;
+  if (g->dtype == MIT_BF16) {
+    if (!mit_gemm_smem_set) {
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_BYTES);
+      mit_gemm_smem_set = true;
+    }
+    if (g->a_layout == 0 && g->b_layout == 0) launch_bf16<0, 0>(g, e, s);
+    else if (g->a_layout == 0 && g->b_layout == 1) launch_bf16<0, 1>(g, e, s);
+    else if (g->a_layout == 1 && g->b_layout == 0) launch_bf16<1, 0>(g, e, s);
+    else launch_bf16<1, 1>(g, e, s);
+  } else {
+    if (g->a_layout == 0 && g->b_layout == 0) launch_f32<0, 0>(g, e, s);
+    else if (g->a_layout == 0 && g->b_layout == 1) launch_f32<0, 1>(g, e, s);
+    else if (g->a_layout == 1 && g->b_layout == 0) launch_f32<1, 0>(g, e, s);
+    else launch_f32<1, 1>(g, e, s);
+  }
+  MIT_LAUNCH_CHECK("mit_gemm");
+  return MIT_OK;
+}

@@ -1,0 +1,397 @@
+// Memory-bound kernels of the train step: encoder input assembly, decoder embedding, cross-entropy,
+// bias-gradient column sums, and the fused clip_grad_norm_ + AdamW optimizer step.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// im2col for the stride == kernel patch Conv2d; one thread per 8 output columns of a patch row
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void im2col_kernel(long B, long C, long H, long W, long P, const float* __restrict__ img, T* __restrict__ out,
+                              long kpad) {
+  const long npw = W / P, nph = H / P, np = nph * npw;
+  const long total = B * np * kpad;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long col = i % kpad, row = i / kpad;
+    const long b = row / np, p = row % np;
+    float v = 0.f;
+    if (col < C * P * P) {
+      const long c = col / (P * P), ky = (col / P) % P, kx = col % P;
+      const long y = (p / npw) * P + ky, x = (p % npw) * P + kx;
+      v = img[((b * C + c) * H + y) * W + x];
+    }
+    out[i] = from_f<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void assemble_kernel(long B, long np, long E, const T* __restrict__ patch, const float* __restrict__ cls,
+                                const float* __restrict__ pos, T* __restrict__ h) {
+  const long total = B * (np + 1) * E;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long e = i % E, t = (i / E) % (np + 1), b = i / (E * (np + 1));
+    const float base = (t == 0) ? cls[e] : to_f(patch[(b * np + t - 1) * E + e]);
+    h[i] = from_f<T>(base + pos[t * E + e]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// decoder embedding
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void embed_fwd_kernel(long B, long T_, long d, const int64_t* __restrict__ tok, const T* __restrict__ table,
+                                 float scale, const float* __restrict__ pe, const uint64_t* seed, uint32_t site,
+                                 uint32_t thresh, float dscale, int dropout, T* __restrict__ out) {
+  const long total = B * T_ * d;
+  const uint64_t key = dropout ? site_key(seed, site) : 0ull;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long c = i % d, bt = i / d, t = bt % T_;
+    const int64_t id = tok[bt];
+    float v = to_f(table[id * d + c]) * scale + pe[t * d + c];
+    if (dropout) v *= drop_mul(key, (uint64_t)i, thresh, dscale);
+    out[i] = from_f<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void embed_bwd_kernel(long B, long T_, long d, const int64_t* __restrict__ tok, const T* __restrict__ dx,
+                                 float scale, const uint64_t* seed, uint32_t site, uint32_t thresh, float dscale,
+                                 int dropout, int pad, float* __restrict__ dtable) {
+  const long total = B * T_ * d;
+  const uint64_t key = dropout ? site_key(seed, site) : 0ull;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long c = i % d, bt = i / d;
+    const int64_t id = tok[bt];
+    if (id == pad) continue;
+    float g = to_f(dx[i]) * scale;
+    if (dropout) g *= drop_mul(key, (uint64_t)i, thresh, dscale);
+    atomicAdd(&dtable[id * d + c], g);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// cross entropy (one 256-thread block per row), in-place gradient
+// ---------------------------------------------------------------------------------------------
+__global__ void count_kernel(const int64_t* __restrict__ t, long n, int ignore, float* count) {
+  __shared__ float scratch[16];
+  float c = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    c += (t[i] != ignore) ? 1.f : 0.f;
+  c = block_sum(c, scratch);
+  if (threadIdx.x == 0) atomicAdd(count, c);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ce_kernel(long V, T* logits, long ld, const int64_t* __restrict__ targets,
+                                                 int ignore, const float* __restrict__ gscale, float* loss_sum,
+                                                 int want_grad) {
+  __shared__ float scratch[16];
+  const long row = blockIdx.x;
+  T* x = logits + row * ld;
+  const int64_t tg = targets[row];
+  const bool ign = (tg == ignore);
+  float mx = -INFINITY;
+  for (long j = threadIdx.x; j < V; j += blockDim.x) mx = fmaxf(mx, to_f(x[j]));
+  mx = block_max(mx, scratch);
+  float se = 0.f;
+  for (long j = threadIdx.x; j < V; j += blockDim.x) se += __expf(to_f(x[j]) - mx);
+  se = block_sum(se, scratch);
+  const float lse = mx + __logf(se);
+  if (threadIdx.x == 0 && !ign) atomicAdd(loss_sum, lse - to_f(x[tg]));
+  if (want_grad) {
+    __syncthreads();  // every thread has read x[tg] above before anyone overwrites it
+    const float gs = ign ? 0.f : *gscale;
+    const float inv = 1.0f / se;
+    for (long j = threadIdx.x; j < V; j += blockDim.x) {
+      float p = __expf(to_f(x[j]) - mx) * inv;
+      if (j == tg) p -= 1.0f;
+      x[j] = from_f<T>(p * gs);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// column sums (bias gradients): partial sums over 128-row chunks, then a reduction over chunks
+// ---------------------------------------------------------------------------------------------
+constexpr long CS_ROWS = 128;
+template <typename T>
+__global__ void colsum_partial(long M, long N, const T* __restrict__ dy, long ld, float* __restrict__ ws) {
+  const long n = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const long r0 = (long)blockIdx.y * CS_ROWS, r1 = min(M, r0 + CS_ROWS);
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) s += to_f(dy[r * ld + n]);
+  ws[blockIdx.y * N + n] = s;
+}
+__global__ void colsum_final(long nch, long N, const float* __restrict__ ws, float* out, int acc) {
+  const long n = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (long c = 0; c < nch; ++c) s += ws[c * N + n];
+  out[n] = acc ? out[n] + s : s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// clip_grad_norm_ + AdamW
+// ---------------------------------------------------------------------------------------------
+constexpr int GN_BLOCKS = 1024;
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, long n, float* __restrict__ ws) {
+  __shared__ float scratch[16];
+  float s = 0.f;
+  const long n4 = n / 4;
+  const f32x4* g4 = (const f32x4*)g;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const f32x4 v = g4[i];
+    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    s += g[i] * g[i];
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) ws[blockIdx.x] = s;
+}
+__global__ void norm_final(const float* __restrict__ ws, int nb, float max_norm, float* out) {
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += (double)ws[i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float total = (float)sqrt(sh[0]);
+    float coef = max_norm / (total + 1e-6f);  // clip_grad.py: clamp(max_norm / (norm + 1e-6), max=1)
+    if (!(coef < 1.0f)) coef = 1.0f;
+    if (max_norm <= 0.f) coef = 1.0f;
+    out[0] = total;
+    out[1] = coef;
+  }
+}
+__global__ void step_inc_kernel(int64_t* step) { *step += 1; }
+
+template <bool SHADOW>
+__global__ __launch_bounds__(256) void adamw_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, bf16* __restrict__ sh,
+                                                    const float* __restrict__ norm_out, const float* __restrict__ lr_p,
+                                                    const int64_t* __restrict__ step_p, float b1, float b2, float eps,
+                                                    float wd) {
+  const float coef = norm_out ? norm_out[1] : 1.0f;
+  const float lr = *lr_p;
+  const double t = (double)*step_p;
+  const float bc1 = (float)(1.0 - pow((double)b1, t));
+  const float bc2 = (float)(1.0 - pow((double)b2, t));
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  const float decay = 1.0f - lr * wd;
+  const long n4 = n / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    f32x4 pp = ((f32x4*)p)[i], gg = ((const f32x4*)g)[i], mm = ((f32x4*)m)[i], vv = ((f32x4*)v)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = gg[k] * coef;
+      pp[k] *= decay;
+      mm[k] = mm[k] + (1.0f - b1) * (gk - mm[k]);
+      vv[k] = vv[k] * b2 + (1.0f - b2) * gk * gk;
+      const float denom = sqrtf(vv[k]) / bc2s + eps;
+      pp[k] = pp[k] - step_size * (mm[k] / denom);
+    }
+    ((f32x4*)p)[i] = pp;
+    ((f32x4*)m)[i] = mm;
+    ((f32x4*)v)[i] = vv;
+    if (SHADOW) {
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      ((bf16x4*)sh)[i] = bf16x4{(bf16)pp[0], (bf16)pp[1], (bf16)pp[2], (bf16)pp[3]};
+    }
+  }
+  for (long i = n4 * 4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float gk = g[i] * coef;
+    float pp = p[i] * decay;
+    const float mm = m[i] + (1.0f - b1) * (gk - m[i]);
+    const float vv = v[i] * b2 + (1.0f - b2) * gk * gk;
+    pp = pp - step_size * (mm / (sqrtf(vv) / bc2s + eps));
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+    if (SHADOW) sh[i] = (bf16)pp;
+  }
+}
+
+template <typename T>
+__global__ void cast_kernel(long n, const float* __restrict__ src, T* __restrict__ dst) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = from_f<T>(src[i]);
+}
+__global__ void mask_kernel(long n, const uint64_t* seed, uint32_t site, uint32_t thresh, float dscale, float* out) {
+  const uint64_t key = site_key(seed, site);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = drop_mul(key, (uint64_t)i, thresh, dscale);
+}
+
+inline unsigned grid_for(long n, int block = 256, long cap = 8192) {
+  long g = (n + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+}  // namespace
+
+#define DISPATCH_T(dtype, ...)        \
+  do {                                \
+    if ((dtype) == MIT_BF16) {        \
+      typedef bf16 T;                 \
+      __VA_ARGS__;                    \
+    } else {                          \
+      typedef float T;                \
+      __VA_ARGS__;                    \
+    }                                 \
+  } while (0)
+
+extern "C" int mit_im2col(int dtype, long B, long C, long H, long W, long P, const float* img, void* out, long kpad,
+                          void* stream) {
+  MIT_CHECK_ARG(img && out && P > 0 && H % P == 0 && W % P == 0 && kpad >= C * P * P, "mit_im2col: bad arguments");
+  const long total = B * (H / P) * (W / P) * kpad;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(im2col_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B,
+                                       C, H, W, P, img, (T*)out, kpad));
+  MIT_LAUNCH_CHECK("mit_im2col");
+  return MIT_OK;
+}
+
+extern "C" int mit_vit_assemble(int dtype, long B, long np, long E, const void* patch, const float* cls,
+                                const float* pos, void* h, void* stream) {
+  MIT_CHECK_ARG(patch && cls && pos && h, "mit_vit_assemble: null pointer");
+  const long total = B * (np + 1) * E;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(assemble_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B,
+                                       np, E, (const T*)patch, cls, pos, (T*)h));
+  MIT_LAUNCH_CHECK("mit_vit_assemble");
+  return MIT_OK;
+}
+
+extern "C" int mit_embed_fwd(int dtype, long B, long T_, long d, const int64_t* tokens, const void* table, float scale,
+                             const float* pe, float drop_p, const uint64_t* seed, uint32_t site, void* out,
+                             void* stream) {
+  MIT_CHECK_ARG(tokens && table && pe && out, "mit_embed_fwd: null pointer");
+  const long total = B * T_ * d;
+  const int dropout = drop_p > 0.f;
+  const uint32_t th = drop_threshold(drop_p);
+  const float sc = drop_p < 1.f ? 1.f / (1.f - drop_p) : 0.f;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(embed_fwd_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                                       B, T_, d, tokens, (const T*)table, scale, pe, seed, site, th, sc, dropout,
+                                       (T*)out));
+  MIT_LAUNCH_CHECK("mit_embed_fwd");
+  return MIT_OK;
+}
+
+extern "C" int mit_embed_bwd(int dtype, long B, long T_, long d, const int64_t* tokens, const void* dx, float scale,
+                             float drop_p, const uint64_t* seed, uint32_t site, int pad_idx, float* dtable,
+                             void* stream) {
+  MIT_CHECK_ARG(tokens && dx && dtable, "mit_embed_bwd: null pointer");
+  const long total = B * T_ * d;
+  const int dropout = drop_p > 0.f;
+  const uint32_t th = drop_threshold(drop_p);
+  const float sc = drop_p < 1.f ? 1.f / (1.f - drop_p) : 0.f;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                                       B, T_, d, tokens, (const T*)dx, scale, seed, site, th, sc, dropout, pad_idx,
+                                       dtable));
+  MIT_LAUNCH_CHECK("mit_embed_bwd");
+  return MIT_OK;
+}
+
+extern "C" int mit_count_targets(const int64_t* targets, long n, int ignore_index, float* count, void* stream) {
+  MIT_CHECK_ARG(targets && count, "mit_count_targets: null pointer");
+  if (n <= 0) return MIT_OK;
+  hipLaunchKernelGGL(count_kernel, dim3(grid_for(n, 256, 64)), dim3(256), 0, (hipStream_t)stream, targets, n,
+                     ignore_index, count);
+  MIT_LAUNCH_CHECK("mit_count_targets");
+  return MIT_OK;
+}
+
+extern "C" int mit_cross_entropy(int dtype, long rows, long V, void* logits, long ld, const int64_t* targets,
+                                 int ignore_index, const float* grad_scale, float* loss_sum, int want_grad,
+                                 void* stream) {
+  MIT_CHECK_ARG(logits && targets && loss_sum && (!want_grad || grad_scale), "mit_cross_entropy: null pointer");
+  MIT_CHECK_ARG(ld >= V, "mit_cross_entropy: ld < V");
+  if (rows <= 0) return MIT_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ce_kernel<T>, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, V,
+                                       (T*)logits, ld, targets, ignore_index, grad_scale, loss_sum, want_grad));
+  MIT_LAUNCH_CHECK("mit_cross_entropy");
+  return MIT_OK;
+}
+
+extern "C" long mit_colsum_ws_floats(long M, long N) { return ((M + CS_ROWS - 1) / CS_ROWS) * N; }
+
+extern "C" int mit_colsum(int dtype, long M, long N, const void* dy, long ld, float* out, int accumulate, float* ws,
+                          void* stream) {
+  MIT_CHECK_ARG(dy && out && ws && ld >= N, "mit_colsum: bad arguments");
+  if (N <= 0) return MIT_OK;
+  const long nch = (M + CS_ROWS - 1) / CS_ROWS;
+  hipStream_t s = (hipStream_t)stream;
+  if (nch > 0) {
+    dim3 grid((unsigned)((N + 255) / 256), (unsigned)nch);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_partial<T>, grid, dim3(256), 0, s, M, N, (const T*)dy, ld, ws));
+    MIT_LAUNCH_CHECK("mit_colsum");
+  }
+  hipLaunchKernelGGL(colsum_final, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, nch, N, ws, out, accumulate);
+  MIT_LAUNCH_CHECK("mit_colsum(final)");
+  return MIT_OK;
+}
+
+extern "C" long mit_grad_norm_ws_floats(long n) { (void)n; return GN_BLOCKS; }
+
+extern "C" int mit_grad_norm(const float* grads, long n, float max_norm, float* ws, float* norm_out, void* stream) {
+  MIT_CHECK_ARG(grads && ws && norm_out, "mit_grad_norm: null pointer");
+  MIT_CHECK_ARG(((uintptr_t)grads % 16) == 0, "mit_grad_norm: grads must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(GN_BLOCKS), dim3(256), 0, s, grads, n, ws);
+  MIT_LAUNCH_CHECK("mit_grad_norm");
+  hipLaunchKernelGGL(norm_final, dim3(1), dim3(256), 0, s, ws, GN_BLOCKS, max_norm, norm_out);
+  MIT_LAUNCH_CHECK("mit_grad_norm(final)");
+  return MIT_OK;
+}
+
+extern "C" int mit_step_inc(int64_t* step, void* stream) {
+  MIT_CHECK_ARG(step, "mit_step_inc: null pointer");
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step);
+  MIT_LAUNCH_CHECK("mit_step_inc");
+  return MIT_OK;
+}
+
+extern "C" int mit_adamw(long n, float* param, const float* grad, float* m, float* v, void* shadow_bf16,
+                         const float* norm_out, const float* lr, const int64_t* step, float beta1, float beta2,
+                         float eps, float weight_decay, void* stream) {
+  MIT_CHECK_ARG(param && grad && m && v && lr && step, "mit_adamw: null pointer");
+  MIT_CHECK_ARG(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
+                "mit_adamw: buffers must be 16-B aligned");
+  MIT_CHECK_ARG(!shadow_bf16 || ((uintptr_t)shadow_bf16 % 8) == 0, "mit_adamw: shadow must be 8-B aligned");
+  if (n <= 0) return MIT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = grid_for(n / 4 + 1, 256, 4096);
+  if (shadow_bf16)
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3(g), dim3(256), 0, s, n, param, grad, m, v, (bf16*)shadow_bf16, norm_out,
+                       lr, step, beta1, beta2, eps, weight_decay);
+  else
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3(g), dim3(256), 0, s, n, param, grad, m, v, (bf16*)nullptr, norm_out,
+                       lr, step, beta1, beta2, eps, weight_decay);
+  MIT_LAUNCH_CHECK("mit_adamw");
+  return MIT_OK;
+}
+
+extern "C" int mit_cast_f32(int dtype, long n, const float* src, void* dst, void* stream) {
+  MIT_CHECK_ARG(src && dst, "mit_cast_f32: null pointer");
+  if (n <= 0) return MIT_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(cast_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, src,
+                                       (T*)dst));
+  MIT_LAUNCH_CHECK("mit_cast_f32");
+  return MIT_OK;
+}
+
+extern "C" int mit_dropout_mask(long n, float p, const uint64_t* seed, uint32_t site, float* out, void* stream) {
+  MIT_CHECK_ARG(out, "mit_dropout_mask: null pointer");
+  if (n <= 0) return MIT_OK;
+  const float sc = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  hipLaunchKernelGGL(mask_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, seed, site,
+                     drop_threshold(p), sc, out);
+  MIT_LAUNCH_CHECK("mit_dropout_mask");
+  return MIT_OK;
+}

@@ -1,0 +1,279 @@
+"""ctypes binding of libmit_hip.so (the C ABI in include/mit_hip.h).
+
+This is the only module that touches the native library. Every wrapper takes torch tensors that
+live on the current HIP device, passes raw pointers / extents / the current stream, and raises
+``NativeError`` with the library's message on a rejected argument or a failed launch.
+
+There is deliberately NO fallback: if the library is missing, or no GPU is present, the first
+call raises. (The CPU oracle lives in /oracle and is test infrastructure only.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MIT_HIP_LIB", os.path.join(_HERE, "lib", "libmit_hip.so"))
+
+F32, BF16 = 0, 1
+K_CONTIG, MN_CONTIG = 0, 1
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_QUICK_GELU = 0, 1, 2, 3
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+vp = ctypes.c_void_p
+L = ctypes.c_long
+I = ctypes.c_int
+Fl = ctypes.c_float
+U32 = ctypes.c_uint32
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [("dtype", I), ("a_layout", I), ("b_layout", I), ("M", L), ("N", L), ("K", L),
+                ("A", vp), ("lda", L), ("B", vp), ("ldb", L), ("C", vp), ("ldc", L), ("alpha", Fl),
+                ("bias", vp), ("act", I), ("residual", vp), ("ldr", L), ("aux", vp), ("ld_aux", L),
+                ("aux_scale", Fl), ("drop_p", Fl), ("seed", vp), ("site", U32), ("out_f32", I),
+                ("accumulate", I)]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [("q", vp), ("q_row", L), ("q_batch", L), ("k", vp), ("k_row", L), ("k_batch", L),
+                ("v", vp), ("v_row", L), ("v_batch", L), ("o", vp), ("o_row", L), ("o_batch", L),
+                ("lse", vp), ("key_tokens", vp), ("tok_batch", L), ("pad_idx", I), ("causal", I),
+                ("scale", Fl), ("drop_p", Fl), ("seed", vp), ("site", U32)]
+
+
+class AttnGrads(ctypes.Structure):
+    _fields_ = [("dout", vp), ("do_row", L), ("do_batch", L), ("dq", vp), ("dq_row", L), ("dq_batch", L),
+                ("dk", vp), ("dk_row", L), ("dk_batch", L), ("dv", vp), ("dv_row", L), ("dv_batch", L),
+                ("delta_ws", vp)]
+
+
+# name -> (restype, argtypes); mirrors include/mit_hip.h one to one
+SIGNATURES = {
+    "mit_last_error": (ctypes.c_char_p, []),
+    "mit_abi_version": (I, []),
+    "mit_gemm": (I, [ctypes.POINTER(GemmArgs), vp]),
+    "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
+    "mit_layernorm_bwd_ws_floats": (L, [L, L]),
+    "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
+    "mit_attention_fwd": (I, [I, L, L, L, L, L, ctypes.POINTER(AttnArgs), vp]),
+    "mit_attention_bwd": (I, [I, L, L, L, L, L, ctypes.POINTER(AttnArgs), ctypes.POINTER(AttnGrads), vp]),
+    "mit_im2col": (I, [I, L, L, L, L, L, vp, vp, L, vp]),
+    "mit_vit_assemble": (I, [I, L, L, L, vp, vp, vp, vp, vp]),
+    "mit_embed_fwd": (I, [I, L, L, L, vp, vp, Fl, vp, Fl, vp, U32, vp, vp]),
+    "mit_embed_bwd": (I, [I, L, L, L, vp, vp, Fl, Fl, vp, U32, I, vp, vp]),
+    "mit_count_targets": (I, [vp, L, I, vp, vp]),
+    "mit_cross_entropy": (I, [I, L, L, vp, L, vp, I, vp, vp, I, vp]),
+    "mit_colsum": (I, [I, L, L, vp, L, vp, I, vp, vp]),
+    "mit_colsum_ws_floats": (L, [L, L]),
+    "mit_grad_norm_ws_floats": (L, [L]),
+    "mit_grad_norm": (I, [vp, L, Fl, vp, vp, vp]),
+    "mit_step_inc": (I, [vp, vp]),
+    "mit_adamw": (I, [L, vp, vp, vp, vp, vp, vp, vp, vp, Fl, Fl, Fl, Fl, vp]),
+    "mit_cast_f32": (I, [I, L, vp, vp, vp]),
+    "mit_dropout_mask": (I, [L, Fl, vp, U32, vp, vp]),
+}
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the HIP library and declare every signature. Raises if the file is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeError(f"libmit_hip.so not found at {path}: build it with `python __graft_entry__.py build` "
+                          f"(or `make -C multimodal-image-transformer_amd/csrc`). There is no CPU fallback.")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib() -> ctypes.CDLL:
+    return _lib if _lib is not None else load_library()
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise NativeError("multimodal-image-transformer_amd kernels need a ROCm GPU (MI355X / gfx950); none is "
+                          "visible. The product path has no CPU fallback.")
+
+
+def _check(rc: int, name: str):
+    if rc != 0:
+        msg = lib().mit_last_error()
+        raise NativeError(f"{name} failed (rc={rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return BF16
+    if t.dtype == torch.float32:
+        return F32
+    raise NativeError(f"unsupported dtype {t.dtype}")
+
+
+# ------------------------------------------------------------------------------------------------
+# thin wrappers
+# ------------------------------------------------------------------------------------------------
+def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ldb=None, ldc=None, bias=None,
+         act=ACT_NONE, residual=None, ldr=None, aux=None, ld_aux=None, aux_scale=1.0, alpha=1.0, drop_p=0.0,
+         seed=None, site=0, accumulate=False):
+    """C = epi(alpha * A(m,k) B(k,n)); see include/mit_hip.h. Output dtype = C.dtype (f32 or operand dtype)."""
+    dt = dtype_code(A)
+    if B.dtype != A.dtype:
+        raise NativeError("gemm: A and B dtypes differ")
+    if C.dtype != A.dtype and C.dtype != torch.float32:
+        raise NativeError("gemm: C must be f32 or the operand dtype")
+    out_f32 = 1 if C.dtype == torch.float32 else 0
+    if lda is None:
+        lda = K if a_layout == K_CONTIG else M
+    if ldb is None:
+        ldb = K if b_layout == K_CONTIG else N
+    if ldc is None:
+        ldc = N
+    g = GemmArgs(dt, a_layout, b_layout, M, N, K, ptr(A), lda, ptr(B), ldb, ptr(C), ldc, alpha, ptr(bias), act,
+                 ptr(residual), ldr if ldr is not None else ldc, ptr(aux), ld_aux if ld_aux is not None else ldc,
+                 aux_scale, drop_p, ptr(seed), site, out_f32, 1 if accumulate else 0)
+    _check(lib().mit_gemm(ctypes.byref(g), stream_ptr()), "mit_gemm")
+
+
+def linear(x, w, out, *, bias=None, act=ACT_NONE, residual=None, drop_p=0.0, seed=None, site=0):
+    """out[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual) — nn.Linear forward."""
+    M, K = x.shape[0], x.shape[-1]
+    N = w.shape[0]
+    gemm(x, w, out, M, N, K, lda=x.stride(0), bias=bias, act=act, residual=residual, drop_p=drop_p, seed=seed,
+         site=site)
+
+
+def layernorm_fwd(x, gamma, beta, eps, y, *, r=None, drop_p=0.0, seed=None, site=0, z=None, mean=None, rstd=None,
+                  rows=None, cols=None, ldx=None, ldy=None):
+    cols = cols if cols is not None else x.shape[-1]
+    rows = rows if rows is not None else x.numel() // cols
+    _check(lib().mit_layernorm_fwd(dtype_code(x), rows, cols, ptr(x), ldx or cols, ptr(r), cols, drop_p, ptr(seed),
+                                   site, ptr(gamma), ptr(beta), eps, ptr(z), ptr(y), ldy or cols, ptr(mean),
+                                   ptr(rstd), stream_ptr()), "mit_layernorm_fwd")
+
+
+def layernorm_bwd_ws_floats(rows, cols):
+    return lib().mit_layernorm_bwd_ws_floats(rows, cols)
+
+
+def layernorm_bwd(dy, z, mean, rstd, gamma, dx, dgamma, dbeta, ws, *, dr=None, drop_p=0.0, seed=None, site=0):
+    cols = z.shape[-1]
+    rows = z.numel() // cols
+    _check(lib().mit_layernorm_bwd(dtype_code(z), rows, cols, ptr(dy), ptr(z), ptr(mean), ptr(rstd), ptr(gamma),
+                                   ptr(dx), ptr(dr), drop_p, ptr(seed), site, ptr(dgamma), ptr(dbeta), ptr(ws),
+                                   stream_ptr()), "mit_layernorm_bwd")
+
+
+def attn_args(q, q_row, q_batch, k, k_row, k_batch, v, v_row, v_batch, o, o_row, o_batch, *, lse=None,
+              key_tokens=None, tok_batch=0, pad_idx=0, causal=False, scale=0.125, drop_p=0.0, seed=None, site=0):
+    return AttnArgs(ptr(q), q_row, q_batch, ptr(k), k_row, k_batch, ptr(v), v_row, v_batch, ptr(o), o_row, o_batch,
+                    ptr(lse), ptr(key_tokens), tok_batch, pad_idx, 1 if causal else 0, scale, drop_p, ptr(seed), site)
+
+
+def attention_fwd(dtype, B, H, Lq, Lk, args: AttnArgs, Dh=64):
+    _check(lib().mit_attention_fwd(dtype, B, H, Lq, Lk, Dh, ctypes.byref(args), stream_ptr()), "mit_attention_fwd")
+
+
+def attention_bwd(dtype, B, H, Lq, Lk, args: AttnArgs, grads: AttnGrads, Dh=64):
+    _check(lib().mit_attention_bwd(dtype, B, H, Lq, Lk, Dh, ctypes.byref(args), ctypes.byref(grads), stream_ptr()),
+           "mit_attention_bwd")
+
+
+def attn_grads(dout, do_row, do_batch, dq, dq_row, dq_batch, dk, dk_row, dk_batch, dv, dv_row, dv_batch, delta_ws):
+    return AttnGrads(ptr(dout), do_row, do_batch, ptr(dq), dq_row, dq_batch, ptr(dk), dk_row, dk_batch, ptr(dv),
+                     dv_row, dv_batch, ptr(delta_ws))
+
+
+def im2col(img, out, patch, kpad):
+    B, C, H, W = img.shape
+    _check(lib().mit_im2col(dtype_code(out), B, C, H, W, patch, ptr(img), ptr(out), kpad, stream_ptr()), "mit_im2col")
+
+
+def vit_assemble(patch_out, cls, pos, h, B, np_, E):
+    _check(lib().mit_vit_assemble(dtype_code(h), B, np_, E, ptr(patch_out), ptr(cls), ptr(pos), ptr(h), stream_ptr()),
+           "mit_vit_assemble")
+
+
+def embed_fwd(tokens, table, scale, pe, out, *, drop_p=0.0, seed=None, site=0):
+    B, T = tokens.shape
+    d = table.shape[1]
+    _check(lib().mit_embed_fwd(dtype_code(out), B, T, d, ptr(tokens), ptr(table), scale, ptr(pe), drop_p, ptr(seed),
+                               site, ptr(out), stream_ptr()), "mit_embed_fwd")
+
+
+def embed_bwd(tokens, dx, scale, dtable, pad_idx, *, drop_p=0.0, seed=None, site=0):
+    B, T = tokens.shape
+    d = dtable.shape[1]
+    _check(lib().mit_embed_bwd(dtype_code(dx), B, T, d, ptr(tokens), ptr(dx), scale, drop_p, ptr(seed), site,
+                               pad_idx, ptr(dtable), stream_ptr()), "mit_embed_bwd")
+
+
+def count_targets(targets, ignore_index, count):
+    _check(lib().mit_count_targets(ptr(targets), targets.numel(), ignore_index, ptr(count), stream_ptr()),
+           "mit_count_targets")
+
+
+def cross_entropy(logits, targets, ignore_index, grad_scale, loss_sum, want_grad, rows=None, V=None, ld=None):
+    V = V if V is not None else logits.shape[-1]
+    rows = rows if rows is not None else targets.numel()
+    _check(lib().mit_cross_entropy(dtype_code(logits), rows, V, ptr(logits), ld or V, ptr(targets), ignore_index,
+                                   ptr(grad_scale), ptr(loss_sum), 1 if want_grad else 0, stream_ptr()),
+           "mit_cross_entropy")
+
+
+def colsum_ws_floats(M, N):
+    return lib().mit_colsum_ws_floats(M, N)
+
+
+def colsum(dy, M, N, out, ws, *, ld=None, accumulate=False):
+    _check(lib().mit_colsum(dtype_code(dy), M, N, ptr(dy), ld or N, ptr(out), 1 if accumulate else 0, ptr(ws),
+                            stream_ptr()), "mit_colsum")
+
+
+def grad_norm_ws_floats(n):
+    return lib().mit_grad_norm_ws_floats(n)
+
+
+def grad_norm(grads, max_norm, ws, norm_out):
+    _check(lib().mit_grad_norm(ptr(grads), grads.numel(), max_norm, ptr(ws), ptr(norm_out), stream_ptr()),
+           "mit_grad_norm")
+
+
+def step_inc(step):
+    _check(lib().mit_step_inc(ptr(step), stream_ptr()), "mit_step_inc")
+
+
+def adamw(param, grad, m, v, shadow, norm_out, lr, step, beta1, beta2, eps, weight_decay):
+    _check(lib().mit_adamw(param.numel(), ptr(param), ptr(grad), ptr(m), ptr(v), ptr(shadow), ptr(norm_out), ptr(lr),
+                           ptr(step), beta1, beta2, eps, weight_decay, stream_ptr()), "mit_adamw")
+
+
+def cast_f32(src, dst):
+    _check(lib().mit_cast_f32(dtype_code(dst), src.numel(), ptr(src), ptr(dst), stream_ptr()), "mit_cast_f32")
+
+
+def dropout_mask(n, p, seed, site, out):
+    _check(lib().mit_dropout_mask(n, p, ptr(seed), site, ptr(out), stream_ptr()), "mit_dropout_mask")

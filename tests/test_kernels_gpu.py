@@ -1,0 +1,313 @@
+"""Per-kernel numerics of libmit_hip.so against plain-PyTorch fp32 references (GPU only).
+
+Tolerances: fp32 kernels ~1e-4 relative; bf16 kernels are compared with the SAME bf16-rounded
+inputs fed to an fp32 reference, tolerance ~1e-2 of the output scale (bf16 output rounding).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+N = None
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    global N
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import native
+    native.load_library()
+    N = native
+    torch.manual_seed(0)
+
+
+def dev():
+    return torch.device("cuda")
+
+
+def _ref_mat(x, layout, rows, cols):
+    """logical [rows, cols] operand from storage (K_CONTIG: stored [rows][cols]; MN: stored [cols][rows])."""
+    return x.float() if layout == 0 else x.float().t()
+
+
+def _close(got, ref, tol):
+    scale = ref.abs().max().item() + 1e-6
+    err = (got.float() - ref).abs().max().item()
+    assert err <= tol * scale, f"max err {err:.3e} vs scale {scale:.3e} (tol {tol})"
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("al,bl", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,Nn,K", [(296, 200, 136), (128, 128, 64), (8, 8, 8), (256, 520, 1000), (72, 64, 124)])
+def test_gemm_layouts(dtype, al, bl, M, Nn, K):
+    if dtype == torch.bfloat16 and K % 8 and (al == 0 or bl == 0):
+        pytest.skip("bf16 K-contiguous operands need K % 8 == 0 (host-checked)")
+    A = torch.randn(M, K, device=dev()) if al == 0 else torch.randn(K, M, device=dev())
+    B = torch.randn(Nn, K, device=dev()) if bl == 0 else torch.randn(K, Nn, device=dev())
+    A, B = A.to(dtype), B.to(dtype)
+    C = torch.empty(M, Nn, device=dev(), dtype=dtype)
+    N.gemm(A, B, C, M, Nn, K, a_layout=al, b_layout=bl)
+    Am = A.float() if al == 0 else A.float().t()
+    Bm = B.float().t() if bl == 0 else B.float()
+    ref = Am @ Bm
+    _close(C, ref, 1e-2 if dtype == torch.bfloat16 else 1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemm_epilogues(dtype):
+    M, Nn, K = 200, 136, 96
+    x = torch.randn(M, K, device=dev()).to(dtype)
+    w = torch.randn(Nn, K, device=dev()).to(dtype) / 10
+    bias = torch.randn(Nn, device=dev())
+    res = torch.randn(M, Nn, device=dev()).to(dtype)
+    base = x.float() @ w.float().t()
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    for act, fn in [(N.ACT_RELU, F.relu), (N.ACT_GELU, F.gelu), (N.ACT_QUICK_GELU, lambda t: t * torch.sigmoid(1.702 * t))]:
+        out = torch.empty(M, Nn, device=dev(), dtype=dtype)
+        N.linear(x, w, out, bias=bias, act=act)
+        _close(out, fn(base + bias), tol)
+    out = torch.empty(M, Nn, device=dev(), dtype=dtype)
+    N.linear(x, w, out, bias=bias, residual=res)
+    _close(out, base + bias + res.float(), tol)
+    # f32 output + accumulate + alpha
+    acc = torch.randn(M, Nn, device=dev())
+    ref = acc + 0.5 * base
+    N.gemm(x, w, acc, M, Nn, K, alpha=0.5, accumulate=True)
+    _close(acc, ref, tol)
+    # aux mask (relu backward): out = base * (aux > 0) * 1.25
+    aux = torch.randn(M, Nn, device=dev()).to(dtype)
+    out = torch.empty(M, Nn, device=dev(), dtype=dtype)
+    N.gemm(x, w, out, M, Nn, K, aux=aux, aux_scale=1.25)
+    _close(out, base * (aux.float() > 0) * 1.25, tol)
+
+
+def test_gemm_rejects_bad_shapes():
+    A = torch.randn(300, 64, device=dev()).to(torch.bfloat16)
+    B = torch.randn(64, 64, device=dev()).to(torch.bfloat16)
+    C = torch.empty(300, 64, device=dev(), dtype=torch.bfloat16)
+    with pytest.raises(N.NativeError, match="multiple"):
+        N.gemm(A, B, C, 300, 64, 64, a_layout=N.MN_CONTIG, lda=300)  # M=300 not a multiple of 8
+
+
+def test_dropout_mask_and_gemm_dropout():
+    seed = torch.tensor([1234], dtype=torch.int64, device=dev())
+    n = 1 << 20
+    m = torch.empty(n, device=dev())
+    N.dropout_mask(n, 0.1, seed, 7, m)
+    keep = (m > 0).float().mean().item()
+    assert abs(keep - 0.9) < 0.003
+    assert torch.allclose(m[m > 0], torch.full_like(m[m > 0], 1 / 0.9))
+    m2 = torch.empty(n, device=dev())
+    N.dropout_mask(n, 0.1, seed, 8, m2)
+    assert (m != m2).float().mean().item() > 0.1  # sites decorrelated
+    # GEMM epilogue dropout == relu(xW^T+b) * mask(site, r*N+c)
+    M, Nn, K = 64, 96, 32
+    x = torch.randn(M, K, device=dev())
+    w = torch.randn(Nn, K, device=dev())
+    b = torch.randn(Nn, device=dev())
+    out = torch.empty(M, Nn, device=dev())
+    N.linear(x, w, out, bias=b, act=N.ACT_RELU, drop_p=0.1, seed=seed, site=3)
+    mk = torch.empty(M * Nn, device=dev())
+    N.dropout_mask(M * Nn, 0.1, seed, 3, mk)
+    ref = F.relu(x @ w.t() + b) * mk.view(M, Nn)
+    _close(out, ref, 1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("cols", [128, 192, 512, 768, 1024])
+def test_layernorm_fwd_bwd(dtype, cols):
+    rows = 200
+    x = torch.randn(rows, cols, device=dev()).to(dtype)
+    r = torch.randn(rows, cols, device=dev()).to(dtype)
+    g = 1 + 0.1 * torch.randn(cols, device=dev())
+    bta = 0.1 * torch.randn(cols, device=dev())
+    y = torch.empty_like(x)
+    z = torch.empty_like(x)
+    mean = torch.empty(rows, device=dev())
+    rstd = torch.empty(rows, device=dev())
+    N.layernorm_fwd(x, g, bta, 1e-5, y, r=r, z=z, mean=mean, rstd=rstd)
+    zr = (x.float() + r.float()).requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = bta.clone().requires_grad_(True)
+    yr = F.layer_norm(zr, (cols,), gr, br, 1e-5)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    _close(y, yr, tol)
+    dy = torch.randn(rows, cols, device=dev()).to(dtype)
+    yr.backward(dy.float())
+    dx = torch.empty_like(x)
+    dr = torch.empty_like(x)
+    dg = torch.zeros(cols, device=dev())
+    db = torch.zeros(cols, device=dev())
+    ws = torch.empty(N.layernorm_bwd_ws_floats(rows, cols), device=dev())
+    N.layernorm_bwd(dy, z, mean, rstd, g, dx, dg, db, ws, dr=dr)
+    _close(dx, zr.grad, 3e-2 if dtype == torch.bfloat16 else 1e-4)
+    _close(dr, zr.grad, 3e-2 if dtype == torch.bfloat16 else 1e-4)
+    _close(dg, gr.grad, 2e-2 if dtype == torch.bfloat16 else 1e-4)
+    _close(db, br.grad, 2e-2 if dtype == torch.bfloat16 else 1e-4)
+
+
+def _attn_ref(q, k, v, causal, kpm, scale, drop=None):
+    # q [B,H,Lq,D]
+    s = (q @ k.transpose(-1, -2)) * scale
+    Lq, Lk = s.shape[-2:]
+    if causal:
+        s = s + torch.triu(torch.full((Lq, Lk), float("-inf"), device=s.device), diagonal=1)
+    if kpm is not None:
+        s = s.masked_fill(kpm[:, None, None, :], float("-inf"))
+    p = torch.softmax(s, -1)
+    lse = torch.logsumexp(s, -1)
+    if drop is not None:
+        p = p * drop
+    return p @ v, lse
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("kind", ["self_causal_pad", "cross", "bidir", "cross_s1", "self_drop"])
+def test_attention_fwd_bwd(dtype, kind):
+    B, H, D = 3, 4, 64
+    if kind == "self_causal_pad" or kind == "self_drop":
+        Lq = Lk = 63
+    elif kind == "cross":
+        Lq, Lk = 63, 197
+    elif kind == "cross_s1":
+        Lq, Lk = 31, 1
+    else:
+        Lq = Lk = 197
+    causal = kind.startswith("self")
+    drop_p = 0.1 if kind == "self_drop" else 0.0
+    q = torch.randn(B, Lq, H * D, device=dev()).to(dtype)
+    kv = torch.randn(B, Lk, 2 * H * D, device=dev()).to(dtype)
+    k, v = kv[..., :H * D], kv[..., H * D:]
+    tok = None
+    kpm = None
+    if causal:
+        tok = torch.randint(4, 100, (B, Lk), device=dev())
+        tok[1, 40:] = 0
+        tok[2, 10:] = 0
+        kpm = tok == 0
+    o = torch.empty(B, Lq, H * D, device=dev(), dtype=dtype)
+    lse = torch.empty(B * H * Lq, device=dev())
+    seed = torch.tensor([99], dtype=torch.int64, device=dev())
+    args = N.attn_args(q, H * D, Lq * H * D, k, 2 * H * D, Lk * 2 * H * D, v, 2 * H * D, Lk * 2 * H * D, o, H * D,
+                       Lq * H * D, lse=lse, key_tokens=tok, tok_batch=Lk, pad_idx=0, causal=causal, scale=0.125,
+                       drop_p=drop_p, seed=seed, site=5)
+    N.attention_fwd(N.dtype_code(q), B, H, Lq, Lk, args)
+    qh = q.float().view(B, Lq, H, D).transpose(1, 2).requires_grad_(True)
+    kh = k.float().reshape(B, Lk, H, D).transpose(1, 2).requires_grad_(True)
+    vh = v.float().reshape(B, Lk, H, D).transpose(1, 2).requires_grad_(True)
+    drop = None
+    if drop_p > 0:
+        mk = torch.empty(B * H * Lq * Lk, device=dev())
+        N.dropout_mask(mk.numel(), drop_p, seed, 5, mk)
+        drop = mk.view(B, H, Lq, Lk)
+    oref, lref = _attn_ref(qh, kh, vh, causal, kpm, 0.125, drop)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    _close(o.view(B, Lq, H, D).transpose(1, 2), oref, tol)
+    _close(lse.view(B, H, Lq), lref, 1e-3 if dtype == torch.bfloat16 else 1e-5)
+    do = torch.randn(B, Lq, H * D, device=dev()).to(dtype)
+    oref.backward(do.float().view(B, Lq, H, D).transpose(1, 2))
+    dq = torch.empty_like(q)
+    dkv = torch.empty_like(kv)
+    delta = torch.empty(B * H * Lq, device=dev())
+    grads = N.attn_grads(do, H * D, Lq * H * D, dq, H * D, Lq * H * D, dkv[..., :H * D], 2 * H * D, Lk * 2 * H * D,
+                         dkv[..., H * D:], 2 * H * D, Lk * 2 * H * D, delta)
+    N.attention_bwd(N.dtype_code(q), B, H, Lq, Lk, args, grads)
+    gt = 4e-2 if dtype == torch.bfloat16 else 2e-4
+    _close(dq.view(B, Lq, H, D).transpose(1, 2), qh.grad, gt)
+    _close(dkv[..., :H * D].reshape(B, Lk, H, D).transpose(1, 2), kh.grad, gt)
+    _close(dkv[..., H * D:].reshape(B, Lk, H, D).transpose(1, 2), vh.grad, gt)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_embed_ce_colsum(dtype):
+    B, T, d, V = 4, 31, 128, 500
+    tok = torch.randint(1, V, (B, T), device=dev())
+    tok[1, 20:] = 0
+    table = torch.randn(V, d, device=dev())
+    pe = torch.randn(100, d, device=dev())
+    out = torch.empty(B, T, d, device=dev(), dtype=dtype)
+    N.embed_fwd(tok, table.to(dtype), math.sqrt(d), pe, out)
+    ref = table.to(dtype).float()[tok] * math.sqrt(d) + pe[:T]
+    _close(out, ref, 1e-2 if dtype == torch.bfloat16 else 1e-6)
+    dx = torch.randn(B, T, d, device=dev()).to(dtype)
+    dtab = torch.zeros(V, d, device=dev())
+    N.embed_bwd(tok, dx, math.sqrt(d), dtab, 0)
+    tr = table.clone().requires_grad_(True)
+    (F.embedding(tok, tr, padding_idx=0) * math.sqrt(d)).backward(dx.float())
+    _close(dtab, tr.grad, 1e-5)
+    # cross entropy with ignore
+    rows = 300
+    logits = torch.randn(rows, V, device=dev()).to(dtype)
+    tgt = torch.randint(0, V, (rows,), device=dev())
+    tgt[::7] = 0
+    cnt = torch.zeros(1, device=dev())
+    N.count_targets(tgt, 0, cnt)
+    assert cnt.item() == (tgt != 0).sum().item()
+    gs = 1.0 / cnt
+    ls = torch.zeros(1, device=dev())
+    lr = logits.float().clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, tgt, ignore_index=0)
+    ref.backward()
+    g = logits.clone()
+    N.cross_entropy(g, tgt, 0, gs, ls, True)
+    assert abs(ls.item() / cnt.item() - ref.item()) < 1e-4 * abs(ref.item()) + 1e-5
+    _close(g, lr.grad, 1e-2 if dtype == torch.bfloat16 else 1e-5)
+    # colsum
+    M, Nn = 1000, 300
+    y = torch.randn(M, Nn, device=dev()).to(dtype)
+    o = torch.empty(Nn, device=dev())
+    ws = torch.empty(N.colsum_ws_floats(M, Nn), device=dev())
+    N.colsum(y, M, Nn, o, ws)
+    _close(o, y.float().sum(0), 1e-5)
+
+
+def test_grad_norm_adamw_matches_torch():
+    n = 100003
+    p = torch.randn(n, device=dev())
+    g = torch.randn(n, device=dev()) * 0.01
+    m = torch.zeros(n, device=dev())
+    v = torch.zeros(n, device=dev())
+    sh = torch.empty(n, device=dev(), dtype=torch.bfloat16)
+    ws = torch.empty(N.grad_norm_ws_floats(n), device=dev())
+    norm = torch.empty(2, device=dev())
+    lr = torch.tensor([1e-3], device=dev())
+    step = torch.zeros(1, dtype=torch.int64, device=dev())
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pr], lr=1e-3, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-5)
+    for it in range(3):
+        gg = g * (it + 1) * 100  # large -> clipping active
+        pr.grad = gg.clone()
+        tn = torch.nn.utils.clip_grad_norm_([pr], 5.0)
+        opt.step()
+        N.grad_norm(gg, 5.0, ws, norm)
+        N.step_inc(step)
+        N.adamw(p, gg, m, v, sh, norm, lr, step, 0.9, 0.98, 1e-9, 1e-5)
+        assert abs(norm[0].item() - tn.item()) < 1e-4 * tn.item()
+    torch.testing.assert_close(p, pr.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(sh.float(), p, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_im2col_patch_embed(dtype):
+    B, C, Hh, P, E = 2, 3, 224, 16, 96
+    img = torch.randn(B, C, Hh, Hh, device=dev())
+    w = torch.randn(E, C, P, P, device=dev()) / 20
+    b = torch.randn(E, device=dev())
+    npch = (Hh // P) ** 2
+    kpad = C * P * P
+    cols = torch.empty(B * npch, kpad, device=dev(), dtype=dtype)
+    N.im2col(img, cols, P, kpad)
+    out = torch.empty(B * npch, E, device=dev(), dtype=dtype)
+    wf = w.reshape(E, -1).to(dtype).contiguous()
+    N.linear(cols, wf, out, bias=b)
+    cls = torch.randn(E, device=dev())
+    pos = torch.randn(npch + 1, E, device=dev())
+    h = torch.empty(B, npch + 1, E, device=dev(), dtype=dtype)
+    N.vit_assemble(out, cls, pos, h, B, npch, E)
+    ref = F.conv2d(img.to(dtype).float(), w.to(dtype).float(), b, stride=P).flatten(2).transpose(1, 2)
+    ref = torch.cat([cls.view(1, 1, E).expand(B, 1, E), ref], 1) + pos
+    _close(h, ref, 2e-2 if dtype == torch.bfloat16 else 1e-4)
