@@ -89,9 +89,8 @@ int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x, long ldx, 
                       float eps, void* z, void* y, long ldy, float* mean, float* rstd, void* stream);
 
 /* Backward of y = LN(z), z = x + dropout(r):
- *   dz = dLN(dy) (+ dy_extra if not NULL, an extra gradient arriving at z... unused: pass NULL)
- *   dx = dz (written to dx, may alias dy), dr = dz * dropout_mask (may be NULL)
- *   dgamma/dbeta: f32 [cols], ACCUMULATED (+=) — the caller zeroes them once per step.
+ *   dx = dz = dLN(dy) (dx may alias dy), dr = dz * dropout_mask (may be NULL)
+ *   dgamma/dbeta: f32 [cols], overwritten.
  *   ws: f32 workspace of >= mit_layernorm_bwd_ws_floats(rows, cols) floats. */
 long mit_layernorm_bwd_ws_floats(long rows, long cols);
 int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy, const void* z, const float* mean,
@@ -170,11 +169,13 @@ int mit_embed_bwd(int dtype, long B, long T, long d, const int64_t* tokens, cons
  * count_targets: *count += #(targets != ignore) as f32 (device scalar, caller zeroes).
  * ce: per row of logits [rows, V] (ld): loss_sum += -log_softmax(row)[t] for t != ignore;
  *     if want_grad, logits are overwritten IN PLACE by d(loss)/d(logits) =
- *     (softmax - onehot) * grad_scale[0], and by 0 for ignored rows. grad_scale is a device scalar
- *     (1 / global non-PAD count: the reference's mean reduction, exact under data parallelism). */
+ *     (softmax - onehot) / count[0], and by 0 for ignored rows. count is a device scalar (the
+ *     GLOBAL non-PAD count: the reference's mean reduction, exact under data parallelism).
+ * scalar_div: out[0] = a[0] / b[0] (mean loss = loss_sum / count, on device, no host sync). */
 int mit_count_targets(const int64_t* targets, long n, int ignore_index, float* count, void* stream);
 int mit_cross_entropy(int dtype, long rows, long V, void* logits, long ld, const int64_t* targets, int ignore_index,
-                      const float* grad_scale, float* loss_sum, int want_grad, void* stream);
+                      const float* count, float* loss_sum, int want_grad, void* stream);
+int mit_scalar_div(const float* a, const float* b, float* out, void* stream);
 
 /* bias gradient: out[n] (+)= sum_m dy[m*ld + n]  (f32 out; accumulate flag) */
 int mit_colsum(int dtype, long M, long N, const void* dy, long ld, float* out, int accumulate, float* ws, void* stream);
@@ -198,6 +199,8 @@ int mit_adamw(long n, float* param, const float* grad, float* m, float* v, void*
  * dropout_mask_debug: writes the keep-multiplier (0 or 1/(1-p)) the kernels use at
  * (seed, site, idx) for idx in [0, n) — tests rebuild reference masks from it. */
 int mit_cast_f32(int dtype, long n, const float* src, void* dst, void* stream);
+/* zero `bytes` bytes at p (hipMemsetAsync on the stream; graph-capturable) */
+int mit_zero(void* p, long bytes, void* stream);
 int mit_dropout_mask(long n, float p, const uint64_t* seed, uint32_t site, float* out, void* stream);
 
 #ifdef __cplusplus

@@ -84,7 +84,7 @@ __global__ void count_kernel(const int64_t* __restrict__ t, long n, int ignore, 
 
 template <typename T>
 __global__ __launch_bounds__(256) void ce_kernel(long V, T* logits, long ld, const int64_t* __restrict__ targets,
-                                                 int ignore, const float* __restrict__ gscale, float* loss_sum,
+                                                 int ignore, const float* __restrict__ count, float* loss_sum,
                                                  int want_grad) {
   __shared__ float scratch[16];
   const long row = blockIdx.x;
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void ce_kernel(long V, T* logits, long ld, con
   if (threadIdx.x == 0 && !ign) atomicAdd(loss_sum, lse - to_f(x[tg]));
   if (want_grad) {
     __syncthreads();  // every thread has read x[tg] above before anyone overwrites it
-    const float gs = ign ? 0.f : *gscale;
+    const float gs = ign ? 0.f : 1.0f / *count;
     const float inv = 1.0f / se;
     for (long j = threadIdx.x; j < V; j += blockDim.x) {
       float p = __expf(to_f(x[j]) - mx) * inv;
@@ -170,6 +170,7 @@ __global__ void norm_final(const float* __restrict__ ws, int nb, float max_norm,
   }
 }
 __global__ void step_inc_kernel(int64_t* step) { *step += 1; }
+__global__ void scalar_div_kernel(const float* a, const float* b, float* out) { *out = *a / *b; }
 
 template <bool SHADOW>
 __global__ __launch_bounds__(256) void adamw_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
@@ -308,13 +309,13 @@ extern "C" int mit_count_targets(const int64_t* targets, long n, int ignore_inde
 }
 
 extern "C" int mit_cross_entropy(int dtype, long rows, long V, void* logits, long ld, const int64_t* targets,
-                                 int ignore_index, const float* grad_scale, float* loss_sum, int want_grad,
+                                 int ignore_index, const float* count, float* loss_sum, int want_grad,
                                  void* stream) {
-  MIT_CHECK_ARG(logits && targets && loss_sum && (!want_grad || grad_scale), "mit_cross_entropy: null pointer");
+  MIT_CHECK_ARG(logits && targets && loss_sum && (!want_grad || count), "mit_cross_entropy: null pointer");
   MIT_CHECK_ARG(ld >= V, "mit_cross_entropy: ld < V");
   if (rows <= 0) return MIT_OK;
   DISPATCH_T(dtype, hipLaunchKernelGGL(ce_kernel<T>, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, V,
-                                       (T*)logits, ld, targets, ignore_index, grad_scale, loss_sum, want_grad));
+                                       (T*)logits, ld, targets, ignore_index, count, loss_sum, want_grad));
   MIT_LAUNCH_CHECK("mit_cross_entropy");
   return MIT_OK;
 }
@@ -393,5 +394,23 @@ extern "C" int mit_dropout_mask(long n, float p, const uint64_t* seed, uint32_t 
   hipLaunchKernelGGL(mask_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, seed, site,
                      drop_threshold(p), sc, out);
   MIT_LAUNCH_CHECK("mit_dropout_mask");
+  return MIT_OK;
+}
+
+extern "C" int mit_scalar_div(const float* a, const float* b, float* out, void* stream) {
+  MIT_CHECK_ARG(a && b && out, "mit_scalar_div: null pointer");
+  hipLaunchKernelGGL(scalar_div_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, a, b, out);
+  MIT_LAUNCH_CHECK("mit_scalar_div");
+  return MIT_OK;
+}
+
+extern "C" int mit_zero(void* p, long bytes, void* stream) {
+  MIT_CHECK_ARG(p || bytes == 0, "mit_zero: null pointer");
+  if (bytes <= 0) return MIT_OK;
+  hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    mit_set_error("mit_zero: %s", hipGetErrorString(e));
+    return MIT_ERR_HIP;
+  }
   return MIT_OK;
 }

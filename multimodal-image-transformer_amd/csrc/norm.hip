@@ -139,8 +139,8 @@ __global__ void ln_param_reduce(long nblk, long cols, const float* __restrict__ 
   if (c >= 2 * cols) return;
   float s = 0.f;
   for (long b = 0; b < nblk; ++b) s += ws[b * 2 * cols + c];
-  if (c < cols) dgamma[c] += s;
-  else dbeta[c - cols] += s;
+  if (c < cols) dgamma[c] = s;
+  else dbeta[c - cols] = s;
 }
 }  // namespace
 

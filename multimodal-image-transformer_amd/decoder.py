@@ -1,0 +1,422 @@
+"""Transformer decoder (reference decoder.py:75-193) with an explicit forward/backward on the
+gfx950 kernels.
+
+Semantics reproduced exactly (post-LN nn.TransformerDecoderLayer, torch/nn/modules/transformer.py
+:1131-1199, built at decoder.py:112-120):
+    x  = dropout(Emb[tok] * sqrt(d) + PE[t])                                  decoder.py:168-171
+    x  = LN1(x + dropout(SelfAttn(x; causal + key-padding mask, attn dropout)))
+    x  = LN2(x + dropout(CrossAttn(x, memory; attn dropout)))
+    x  = LN3(x + dropout(W2 dropout(relu(W1 x + b1)) + b2))
+    logits = x Wfc^T + bfc                                                   decoder.py:191
+MHA uses a packed in_proj (q,k,v rows), scale 1/sqrt(head_dim) (torch/nn/functional.py:6435).
+
+MI355X-specific layout decisions:
+  * the cross-attention K/V projections of ALL layers only depend on the memory, so they are one
+    GEMM  kv_all[B*S, L*2d] = memory @ W_kv_all^T  (N = 6144 at cfg1) in the forward, and one
+    dW GEMM + one dX GEMM in the backward (the reference issues 2 x L smaller ones);
+  * the masks are never materialised (computed in-kernel from tokens == PAD and j > i);
+  * dropout masks are regenerated from (seed, site, index) in the backward, never stored;
+  * weight gradients are written ONCE (no zero-fill + accumulate), straight into the flat f32
+    gradient buffer (params.FlatParams) in backward-completion order.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+import native
+from params import FlatParams
+
+EMB_SITE = 4000
+
+
+def sinusoidal_pe(max_len: int, d: int) -> torch.Tensor:
+    """The PositionalEncodingBatchFirst buffer (decoder.py:34-47), [max_len, d] f32."""
+    pos = torch.arange(max_len).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2) * (-math.log(10000.0) / d))
+    pe = torch.zeros(max_len, d)
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe
+
+
+def decoder_entries(V: int, d: int, L: int, F: int, proj_in: Optional[int]) -> List[Tuple[str, Tuple[int, ...]]]:
+    """Flat-buffer layout in backward-completion order (see params.py)."""
+    e = [("fc_out.weight", (V, d)), ("fc_out.bias", (V,))]
+    for i in reversed(range(L)):
+        p = f"layers.{i}."
+        e += [(p + "linear2.weight", (d, F)), (p + "linear2.bias", (d,)), (p + "linear1.weight", (F, d)),
+              (p + "linear1.bias", (F,)), (p + "norm3.weight", (d,)), (p + "norm3.bias", (d,)),
+              (p + "cross_out.weight", (d, d)), (p + "cross_out.bias", (d,)), (p + "cross_q.weight", (d, d)),
+              (p + "cross_q.bias", (d,)), (p + "norm2.weight", (d,)), (p + "norm2.bias", (d,)),
+              (p + "self_out.weight", (d, d)), (p + "self_out.bias", (d,)), (p + "self_in.weight", (3 * d, d)),
+              (p + "self_in.bias", (3 * d,)), (p + "norm1.weight", (d,)), (p + "norm1.bias", (d,))]
+    e += [("cross_kv.weight", (L * 2 * d, d)), ("cross_kv.bias", (L * 2 * d,)), ("token_embedding.weight", (V, d))]
+    if proj_in is not None:
+        e += [("projection.weight", (d, proj_in)), ("projection.bias", (d,))]
+    return e
+
+
+def reference_to_flat(sd: Dict[str, torch.Tensor], L: int, d: int, prefix: str = "decoder.") -> Dict[str, torch.Tensor]:
+    """Reference state_dict names (decoder.* / projection.*) -> flat entry names."""
+    out = {}
+    kv_w, kv_b = [None] * L, [None] * L
+    for k, v in sd.items():
+        if k.startswith("projection."):
+            out[k] = v
+            continue
+        if not k.startswith(prefix):
+            continue
+        k = k[len(prefix):]
+        if k in ("fc_out.weight", "fc_out.bias", "token_embedding.weight"):
+            out[k] = v
+        elif k.startswith("transformer_decoder.layers."):
+            rest = k[len("transformer_decoder.layers."):]
+            i, sub = rest.split(".", 1)
+            i = int(i)
+            p = f"layers.{i}."
+            if sub == "self_attn.in_proj_weight":
+                out[p + "self_in.weight"] = v
+            elif sub == "self_attn.in_proj_bias":
+                out[p + "self_in.bias"] = v
+            elif sub.startswith("self_attn.out_proj."):
+                out[p + "self_out." + sub.rsplit(".", 1)[1]] = v
+            elif sub == "multihead_attn.in_proj_weight":
+                out[p + "cross_q.weight"] = v[:d]
+                kv_w[i] = v[d:]
+            elif sub == "multihead_attn.in_proj_bias":
+                out[p + "cross_q.bias"] = v[:d]
+                kv_b[i] = v[d:]
+            elif sub.startswith("multihead_attn.out_proj."):
+                out[p + "cross_out." + sub.rsplit(".", 1)[1]] = v
+            else:  # linear1/linear2/norm1-3
+                out[p + sub] = v
+    if all(x is not None for x in kv_w):
+        out["cross_kv.weight"] = torch.cat(kv_w, 0)
+    if all(x is not None for x in kv_b):
+        out["cross_kv.bias"] = torch.cat(kv_b, 0)
+    return out
+
+
+def flat_to_reference(store: FlatParams, L: int, d: int, prefix: str = "decoder.") -> Dict[str, torch.Tensor]:
+    """Inverse of reference_to_flat: the reference's state_dict keys (§8b), f32 copies."""
+    sd = {}
+    p = lambda n: store.p(n).detach().clone()  # noqa: E731
+    kvw, kvb = store.p("cross_kv.weight"), store.p("cross_kv.bias")
+    sd[prefix + "token_embedding.weight"] = p("token_embedding.weight")
+    for i in range(L):
+        r, q = f"{prefix}transformer_decoder.layers.{i}.", f"layers.{i}."
+        sd[r + "self_attn.in_proj_weight"] = p(q + "self_in.weight")
+        sd[r + "self_attn.in_proj_bias"] = p(q + "self_in.bias")
+        sd[r + "self_attn.out_proj.weight"] = p(q + "self_out.weight")
+        sd[r + "self_attn.out_proj.bias"] = p(q + "self_out.bias")
+        sd[r + "multihead_attn.in_proj_weight"] = torch.cat([p(q + "cross_q.weight"), kvw[i * 2 * d:(i + 1) * 2 * d]], 0)
+        sd[r + "multihead_attn.in_proj_bias"] = torch.cat([p(q + "cross_q.bias"), kvb[i * 2 * d:(i + 1) * 2 * d]], 0)
+        sd[r + "multihead_attn.out_proj.weight"] = p(q + "cross_out.weight")
+        sd[r + "multihead_attn.out_proj.bias"] = p(q + "cross_out.bias")
+        for s in ("linear1", "linear2", "norm1", "norm2", "norm3"):
+            sd[r + s + ".weight"] = p(q + s + ".weight")
+            sd[r + s + ".bias"] = p(q + s + ".bias")
+    sd[prefix + "fc_out.weight"] = p("fc_out.weight")
+    sd[prefix + "fc_out.bias"] = p("fc_out.bias")
+    return sd
+
+
+class _Acts:
+    """Activation arena for one (B, T, S, train) shape; allocated once, reused every step."""
+
+    def __init__(self, B, T, S, d, F, L, V, H, dt, dev, train: bool):
+        R = B * T
+        e = lambda *s: torch.empty(*s, dtype=dt, device=dev)  # noqa: E731
+        f = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.R = R
+        self.x0 = e(R, d)
+        self.y = e(R, d)
+        self.kv = e(B * S, L * 2 * d)
+        self.logits = e(R, V)
+        nl = L if train else 1  # eval keeps one set of per-layer buffers and reuses it
+        self.qkv = [e(R, 3 * d) for _ in range(nl)]
+        self.os = [e(R, d) for _ in range(nl)]
+        self.oc = [e(R, d) for _ in range(nl)]
+        self.qc = [e(R, d) for _ in range(nl)]
+        self.h = [e(R, F) for _ in range(nl)]
+        self.z = [[e(R, d) for _ in range(3)] for _ in range(nl)]
+        self.st = [[(f(R), f(R)) for _ in range(3)] for _ in range(nl)]
+        self.lse_s = [f(B * H * T) for _ in range(nl)]
+        self.lse_c = [f(B * H * T) for _ in range(nl)]
+        # per-layer normalised outputs x1, x2, x3 (x3 of layer l = input of layer l+1)
+        self.xs = [[e(R, d) for _ in range(3)] for _ in range(L if train else 2)]
+        self.count = f(1)
+        self.loss_sum = f(1)
+        self.loss = f(1)
+        if train:
+            self.dx = e(R, d)
+            self.dy = e(R, d)
+            self.do = e(R, d)
+            self.dq = e(R, d)
+            self.dqkv = e(R, 3 * d)
+            self.dh = e(R, F)
+            self.dkv = e(B * S, L * 2 * d)
+            self.dmem = e(B * S, d)
+            self.delta = f(B * H * T)
+            self.ln_ws = f(native.layernorm_bwd_ws_floats(R, d))
+            self.cs_ws = f(max(native.colsum_ws_floats(R, max(V, F, 3 * d)),
+                               native.colsum_ws_floats(B * S, L * 2 * d)))
+
+
+class TransformerDecoder:
+    """Reference-surface decoder: same constructor arguments as decoder.py:84-85.
+
+    Parameters live in a FlatParams store (shared with the model's projection when built by
+    model.ImageToTextModel). ``forward(tgt_tokens, memory, memory_padding_mask=None)`` matches
+    decoder.py:134-193 and returns f32 logits [B, T, V].
+    """
+
+    def __init__(self, vocab_size: int, embed_dim: int, num_heads: int, num_layers: int, ff_dim: int,
+                 max_seq_len: int, dropout: float = 0.1, pad_idx: int = 0, *, store: Optional[FlatParams] = None,
+                 device=None, dtype: Optional[torch.dtype] = None):
+        native.require_gpu()
+        self.V, self.d, self.H, self.L, self.F = vocab_size, embed_dim, num_heads, num_layers, ff_dim
+        if embed_dim % num_heads or embed_dim // num_heads != 64:
+            raise ValueError(f"head_dim {embed_dim / num_heads} unsupported: the attention kernels are head_dim 64")
+        self.max_seq_len, self.dropout, self.pad_idx = max_seq_len, dropout, pad_idx
+        self.embed_dim = embed_dim
+        self.device = device or torch.device("cuda")
+        if store is None:
+            dt = dtype or torch.bfloat16
+            store = FlatParams(decoder_entries(vocab_size, embed_dim, num_layers, ff_dim, None), self.device, dt)
+            self._own_store = True
+        else:
+            self._own_store = False
+        self.store = store
+        self.dtype = store.compute_dtype
+        self.pe = sinusoidal_pe(max_seq_len, embed_dim).to(self.device)
+        self.training = True
+        self._acts: Dict[tuple, _Acts] = {}
+        if self._own_store:
+            self.init_weights(0)
+
+    # --- weights -----------------------------------------------------------------------------
+    def init_weights(self, seed: int = 0):
+        """decoder.py:128-132: xavier_uniform_ on every >=2-D weight (embedding included, so the
+        PAD row is not zero); MHA in/out-proj biases 0 (torch/nn/modules/activation.py:1241-1242);
+        LayerNorm 1/0; Linear biases U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (nn.Linear default)."""
+        g = torch.Generator().manual_seed(seed)
+        d, L = self.d, self.L
+        for name, shape, _, _ in self.store.entries:
+            if name.startswith("projection."):
+                continue
+            if name == "cross_kv.weight":
+                # xavier on each layer's full in_proj [3d, d] (fan_out = 3d), restricted to the kv rows
+                a = math.sqrt(6.0 / (3 * d + d))
+                t = (torch.rand(*shape, generator=g) * 2 - 1) * a
+            elif len(shape) == 2:
+                fo, fi = shape
+                if name.endswith("cross_q.weight"):
+                    fo = 3 * d
+                a = math.sqrt(6.0 / (fo + fi))
+                t = (torch.rand(*shape, generator=g) * 2 - 1) * a
+            elif "norm" in name:
+                t = torch.ones(shape) if name.endswith("weight") else torch.zeros(shape)
+            elif any(s in name for s in ("self_in.bias", "self_out.bias", "cross_q.bias", "cross_out.bias",
+                                          "cross_kv.bias")):
+                t = torch.zeros(shape)
+            else:  # linear1/linear2/fc_out biases
+                fan_in = {"linear1.bias": d, "linear2.bias": self.F, "fc_out.bias": d}[name.split(".", 2)[-1]
+                                                                                        if name.startswith("layers.")
+                                                                                        else name]
+                b = 1 / math.sqrt(fan_in)
+                t = (torch.rand(*shape, generator=g) * 2 - 1) * b
+            self.store.p(name).copy_(t)
+        self.store.sync_shadow()
+
+    def train(self, mode: bool = True):
+        self.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    # --- forward -----------------------------------------------------------------------------
+    def acts(self, B, T, S, train) -> _Acts:
+        key = (B, T, S, train)
+        if key not in self._acts:
+            self._acts[key] = _Acts(B, T, S, self.d, self.F, self.L, self.V, self.H, self.dtype, self.device, train)
+        return self._acts[key]
+
+    def _p(self):
+        return self.dropout if self.training else 0.0
+
+    def run_forward(self, tokens: torch.Tensor, mem: torch.Tensor, mem_ld: int, S: int, A: _Acts,
+                    seed: Optional[torch.Tensor], train: bool, logits_out: Optional[torch.Tensor] = None,
+                    drop_p: Optional[float] = None):
+        """tokens int64 [B,T] (device); mem: memory rows [B*S, d] with row stride mem_ld.
+        train=True keeps every layer's activations for run_backward (A must be a train arena);
+        drop_p defaults to the module's dropout in train mode and 0 otherwise."""
+        B, T = tokens.shape
+        d, H, L, V = self.d, self.H, self.L, self.V
+        st = self.store
+        p = drop_p if drop_p is not None else (self._p() if train else 0.0)
+        w = st.w
+        R = B * T
+        # fused cross-attention K/V projection of every layer (decoder-layer independent)
+        native.gemm(mem, w("cross_kv.weight"), A.kv, B * S, L * 2 * d, d, lda=mem_ld, bias=st.p("cross_kv.bias"))
+        native.embed_fwd(tokens, w("token_embedding.weight"), math.sqrt(d), self.pe, A.x0, drop_p=p, seed=seed,
+                         site=EMB_SITE)
+        xin = A.x0
+        for l in range(L):
+            j = l if train else 0
+            xs = A.xs[l] if train else A.xs[l % 2]
+            z, stt = A.z[j], A.st[j]
+            pre = f"layers.{l}."
+            base = 64 * l
+            qkv = A.qkv[j]
+            native.linear(xin, w(pre + "self_in.weight"), qkv, bias=st.p(pre + "self_in.bias"))
+            sa = native.attn_args(qkv, 3 * d, T * 3 * d, qkv[:, d:], 3 * d, T * 3 * d, qkv[:, 2 * d:], 3 * d, T * 3 * d,
+                                  A.os[j], d, T * d, lse=A.lse_s[j], key_tokens=tokens, tok_batch=T,
+                                  pad_idx=self.pad_idx, causal=True, scale=1.0 / math.sqrt(64), drop_p=p, seed=seed,
+                                  site=base + 0)
+            native.attention_fwd(native.dtype_code(qkv), B, H, T, T, sa)
+            native.linear(A.os[j], w(pre + "self_out.weight"), A.y, bias=st.p(pre + "self_out.bias"))
+            native.layernorm_fwd(xin, st.p(pre + "norm1.weight"), st.p(pre + "norm1.bias"), 1e-5, xs[0], r=A.y,
+                                 drop_p=p, seed=seed, site=base + 1, z=z[0], mean=stt[0][0], rstd=stt[0][1])
+            native.linear(xs[0], w(pre + "cross_q.weight"), A.qc[j], bias=st.p(pre + "cross_q.bias"))
+            kvl = A.kv[:, l * 2 * d:]
+            ca = native.attn_args(A.qc[j], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
+                                  S * L * 2 * d, A.oc[j], d, T * d, lse=A.lse_c[j], scale=1.0 / math.sqrt(64), drop_p=p,
+                                  seed=seed, site=base + 2)
+            native.attention_fwd(native.dtype_code(qkv), B, H, T, S, ca)
+            native.linear(A.oc[j], w(pre + "cross_out.weight"), A.y, bias=st.p(pre + "cross_out.bias"))
+            native.layernorm_fwd(xs[0], st.p(pre + "norm2.weight"), st.p(pre + "norm2.bias"), 1e-5, xs[1], r=A.y,
+                                 drop_p=p, seed=seed, site=base + 3, z=z[1], mean=stt[1][0], rstd=stt[1][1])
+            native.linear(xs[1], w(pre + "linear1.weight"), A.h[j], bias=st.p(pre + "linear1.bias"),
+                          act=native.ACT_RELU, drop_p=p, seed=seed, site=base + 4)
+            native.linear(A.h[j], w(pre + "linear2.weight"), A.y, bias=st.p(pre + "linear2.bias"))
+            native.layernorm_fwd(xs[1], st.p(pre + "norm3.weight"), st.p(pre + "norm3.bias"), 1e-5, xs[2], r=A.y,
+                                 drop_p=p, seed=seed, site=base + 5, z=z[2], mean=stt[2][0], rstd=stt[2][1])
+            xin = xs[2]
+        logits = A.logits if logits_out is None else logits_out
+        native.linear(xin, w("fc_out.weight"), logits, bias=st.p("fc_out.bias"))
+        return logits, xin
+
+    def run_backward(self, tokens: torch.Tensor, mem: torch.Tensor, mem_ld: int, S: int, A: _Acts,
+                     seed: Optional[torch.Tensor], dlogits: torch.Tensor,
+                     proj_input: Optional[Tuple[torch.Tensor, int, int]] = None,
+                     grads_ready: Optional[Callable[[str, str], None]] = None):
+        """Backward of run_forward(train=True) given dlogits [R, V] (compute dtype).
+        proj_input = (enc_rows, ld, E): encoder features feeding the projection (for dW_proj).
+        grads_ready(first, last) is called as soon as the grads of a contiguous entry span are final."""
+        B, T = tokens.shape
+        d, H, L, V, F = self.d, self.H, self.L, self.V, self.F
+        st, p = self.store, self._p()
+        w, g = st.w, st.g
+        R = B * T
+        MN, K = native.MN_CONTIG, native.K_CONTIG
+        x_last = A.xs[L - 1][2]
+        # fc_out
+        native.gemm(dlogits, x_last, g("fc_out.weight"), V, d, R, a_layout=MN, b_layout=MN, lda=V, ldb=d)
+        native.colsum(dlogits, R, V, g("fc_out.bias"), A.cs_ws)
+        native.gemm(dlogits, w("fc_out.weight"), A.dx, R, d, V, b_layout=MN, ldb=d)
+        if grads_ready:
+            grads_ready("fc_out.weight", "fc_out.bias")
+        ascale = 1.0 / (1.0 - p) if p > 0 else 1.0
+        for l in reversed(range(L)):
+            pre = f"layers.{l}."
+            base = 64 * l
+            xs, z, stt = A.xs[l], A.z[l], A.st[l]
+            xin = A.x0 if l == 0 else A.xs[l - 1][2]
+            # LN3 -> dz3 (dx, in place) and d(ffn_out) (dy)
+            native.layernorm_bwd(A.dx, z[2], stt[2][0], stt[2][1], st.p(pre + "norm3.weight"), A.dx,
+                                 g(pre + "norm3.weight"), g(pre + "norm3.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
+                                 site=base + 5)
+            # FFN
+            native.gemm(A.dy, A.h[l], g(pre + "linear2.weight"), d, F, R, a_layout=MN, b_layout=MN, lda=d, ldb=F)
+            native.colsum(A.dy, R, d, g(pre + "linear2.bias"), A.cs_ws)
+            native.gemm(A.dy, w(pre + "linear2.weight"), A.dh, R, F, d, b_layout=MN, ldb=F, aux=A.h[l], ld_aux=F,
+                        aux_scale=ascale)
+            native.gemm(A.dh, xs[1], g(pre + "linear1.weight"), F, d, R, a_layout=MN, b_layout=MN, lda=F, ldb=d)
+            native.colsum(A.dh, R, F, g(pre + "linear1.bias"), A.cs_ws)
+            native.gemm(A.dh, w(pre + "linear1.weight"), A.dx, R, d, F, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
+            # LN2
+            native.layernorm_bwd(A.dx, z[1], stt[1][0], stt[1][1], st.p(pre + "norm2.weight"), A.dx,
+                                 g(pre + "norm2.weight"), g(pre + "norm2.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
+                                 site=base + 3)
+            # cross-attention block
+            native.gemm(A.dy, A.oc[l], g(pre + "cross_out.weight"), d, d, R, a_layout=MN, b_layout=MN, lda=d, ldb=d)
+            native.colsum(A.dy, R, d, g(pre + "cross_out.bias"), A.cs_ws)
+            native.gemm(A.dy, w(pre + "cross_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d)
+            kvl, dkvl = A.kv[:, l * 2 * d:], A.dkv[:, l * 2 * d:]
+            ca = native.attn_args(A.qc[l], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
+                                  S * L * 2 * d, A.oc[l], d, T * d, lse=A.lse_c[l], scale=1.0 / math.sqrt(64), drop_p=p,
+                                  seed=seed, site=base + 2)
+            cg = native.attn_grads(A.do, d, T * d, A.dq, d, T * d, dkvl, L * 2 * d, S * L * 2 * d, dkvl[:, d:],
+                                   L * 2 * d, S * L * 2 * d, A.delta)
+            native.attention_bwd(native.dtype_code(A.dq), B, H, T, S, ca, cg)
+            native.gemm(A.dq, xs[0], g(pre + "cross_q.weight"), d, d, R, a_layout=MN, b_layout=MN, lda=d, ldb=d)
+            native.colsum(A.dq, R, d, g(pre + "cross_q.bias"), A.cs_ws)
+            native.gemm(A.dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
+            # LN1
+            native.layernorm_bwd(A.dx, z[0], stt[0][0], stt[0][1], st.p(pre + "norm1.weight"), A.dx,
+                                 g(pre + "norm1.weight"), g(pre + "norm1.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
+                                 site=base + 1)
+            # self-attention block
+            native.gemm(A.dy, A.os[l], g(pre + "self_out.weight"), d, d, R, a_layout=MN, b_layout=MN, lda=d, ldb=d)
+            native.colsum(A.dy, R, d, g(pre + "self_out.bias"), A.cs_ws)
+            native.gemm(A.dy, w(pre + "self_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d)
+            qkv = A.qkv[l]
+            sa = native.attn_args(qkv, 3 * d, T * 3 * d, qkv[:, d:], 3 * d, T * 3 * d, qkv[:, 2 * d:], 3 * d, T * 3 * d,
+                                  A.os[l], d, T * d, lse=A.lse_s[l], key_tokens=tokens, tok_batch=T,
+                                  pad_idx=self.pad_idx, causal=True, scale=1.0 / math.sqrt(64), drop_p=p, seed=seed,
+                                  site=base + 0)
+            sg = native.attn_grads(A.do, d, T * d, A.dqkv, 3 * d, T * 3 * d, A.dqkv[:, d:], 3 * d, T * 3 * d,
+                                   A.dqkv[:, 2 * d:], 3 * d, T * 3 * d, A.delta)
+            native.attention_bwd(native.dtype_code(A.dq), B, H, T, T, sa, sg)
+            native.gemm(A.dqkv, xin, g(pre + "self_in.weight"), 3 * d, d, R, a_layout=MN, b_layout=MN, lda=3 * d, ldb=d)
+            native.colsum(A.dqkv, R, 3 * d, g(pre + "self_in.bias"), A.cs_ws)
+            native.gemm(A.dqkv, w(pre + "self_in.weight"), A.dx, R, d, 3 * d, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
+            if grads_ready:
+                grads_ready(pre + "linear2.weight", pre + "norm1.bias")
+        # cross K/V of all layers
+        BS = B * S
+        native.gemm(A.dkv, mem, g("cross_kv.weight"), L * 2 * d, d, BS, a_layout=MN, b_layout=MN, lda=L * 2 * d,
+                    ldb=mem_ld)
+        native.colsum(A.dkv, BS, L * 2 * d, g("cross_kv.bias"), A.cs_ws)
+        # embedding (scatter-add into a zeroed table gradient; PAD row gets nothing)
+        ge = g("token_embedding.weight")
+        native.zero(ge)
+        native.embed_bwd(tokens, A.dx, math.sqrt(d), ge, self.pad_idx, drop_p=p, seed=seed, site=EMB_SITE)
+        last = "token_embedding.weight"
+        if proj_input is not None:
+            enc_rows, enc_ld, E = proj_input
+            native.gemm(A.dkv, w("cross_kv.weight"), A.dmem, BS, d, L * 2 * d, b_layout=MN, ldb=d)
+            native.gemm(A.dmem, enc_rows, g("projection.weight"), d, E, BS, a_layout=MN, b_layout=MN, lda=d,
+                        ldb=enc_ld)
+            native.colsum(A.dmem, BS, d, g("projection.bias"), A.cs_ws)
+            last = "projection.bias"
+        if grads_ready:
+            grads_ready("cross_kv.weight", last)
+
+    def forward(self, tgt_tokens: torch.Tensor, memory: torch.Tensor, memory_padding_mask=None) -> torch.Tensor:
+        """decoder.py:134-193: f32 logits [B, T, V] (no autograd; training goes through the model's
+        fused train step)."""
+        if memory_padding_mask is not None:
+            raise NotImplementedError("memory_padding_mask: the reference never passes one (model.py:158)")
+        tokens = tgt_tokens.to(self.device, torch.int64).contiguous()
+        B, T = tokens.shape
+        S = memory.shape[1]
+        mem = memory.to(self.device, self.dtype).reshape(B * S, self.d).contiguous()
+        A = self.acts(B, T, S, False)
+        out = torch.empty(B * T, self.V, dtype=torch.float32, device=self.device)
+        self.run_forward(tokens, mem, self.d, S, A, None, False, logits_out=out)
+        return out.view(B, T, self.V)
+
+    __call__ = forward
+
+    def flops_per_sequence(self, T: int, S: int) -> float:
+        """Algorithmic forward FLOPs for one caption (SURVEY.md §8d convention)."""
+        d, F, V, L = self.d, self.F, self.V, self.L
+        layer = 2 * T * 3 * d * d + 2 * T * d * d + 4 * T * T * d + 2 * T * d * d + 2 * S * 2 * d * d + 4 * T * S * d \
+            + 2 * T * d * d + 2 * T * 2 * d * F
+        return L * layer + 2 * T * d * V

@@ -1,0 +1,276 @@
+"""Frozen vision encoder (ViT / CLIP vision tower), forward only, on the gfx950 kernels.
+
+Replaces the HF modules the reference loads in model.py:48-66 and calls at model.py:133-141:
+  ViT  (tf/models/vit/modeling_vit.py:356-389): Conv2d patch embed + CLS + position embeddings,
+       pre-LN layers (LN eps 1e-12, MHSA scale 1/8, GELU(erf) MLP), final LayerNorm.
+  CLIP (tf/models/clip/modeling_clip.py:613-657): bias-free patch conv, class + position embeddings,
+       pre_layrnorm, pre-LN layers with quick_gelu, NO post-LN on last_hidden_state.
+The pooler (modeling_vit.py:386) is not observable through last_hidden_state and is not computed.
+
+Per layer: LN -> one packed QKV GEMM (N = 3E) -> attention -> o_proj GEMM with the residual add
+fused in its epilogue -> LN -> fc1 GEMM with GELU fused -> fc2 GEMM with the residual fused.
+Weights live in the compute dtype (bf16 or f32); biases and LN parameters in f32.
+
+Also the counterpart of the reference's standalone encoder.py helpers (encoder.py:65-124):
+``get_encoder_output_dim`` and ``encode_image``.
+"""
+from __future__ import annotations
+
+import math
+import re
+from typing import Dict, Optional
+
+import torch
+
+import config
+import native
+
+
+def _round8(x):
+    return (x + 7) // 8 * 8
+
+
+def _normalize_hf_key(k: str) -> str:
+    """Map HF ViT/CLIP vision state_dict names (transformers 4.x or 5.x, with or without the
+    'encoder.' / 'vision_model.' prefixes the reference's checkpoints carry) to one scheme."""
+    for pre in ("encoder.vision_model.", "vision_model.", "encoder."):
+        if k.startswith(pre) and not k.startswith(("encoder.layer.", "encoder.layers.")):
+            k = k[len(pre):]
+            break
+    if k.startswith("encoder.") and k[len("encoder."):].startswith(("layer.", "layers.")):
+        k = k[len("encoder."):]
+    k = re.sub(r"^layer\.", "layers.", k)
+    # transformers 4.x ViT
+    k = k.replace("attention.attention.query", "attention.q_proj").replace("attention.attention.key", "attention.k_proj")
+    k = k.replace("attention.attention.value", "attention.v_proj").replace("attention.output.dense", "attention.o_proj")
+    k = k.replace("intermediate.dense", "mlp.fc1")
+    k = re.sub(r"(layers\.\d+)\.output\.dense", r"\1.mlp.fc2", k)
+    # CLIP names -> ViT-style names
+    k = k.replace("self_attn.q_proj", "attention.q_proj").replace("self_attn.k_proj", "attention.k_proj")
+    k = k.replace("self_attn.v_proj", "attention.v_proj").replace("self_attn.out_proj", "attention.o_proj")
+    k = k.replace("layer_norm1", "layernorm_before").replace("layer_norm2", "layernorm_after")
+    return k
+
+
+class VisionEncoder:
+    """Frozen encoder. ``spec`` = config.ENCODER_SPECS entry (kind, hidden, layers, heads, mlp, image, patch, eps)."""
+
+    def __init__(self, spec: dict, device, dtype: torch.dtype):
+        self.spec = dict(spec)
+        self.kind = spec["kind"]
+        self.E, self.L, self.H, self.mlp = spec["hidden"], spec["layers"], spec["heads"], spec["mlp"]
+        self.image, self.patch, self.eps = spec["image"], spec["patch"], spec["eps"]
+        if self.E % self.H or self.E // self.H != 64:
+            raise ValueError(f"encoder head_dim {self.E / self.H} unsupported (kernels are head_dim 64)")
+        self.np = (self.image // self.patch) ** 2
+        self.N = self.np + 1
+        self.kin = 3 * self.patch * self.patch
+        self.kpad = _round8(self.kin)
+        self.device, self.dtype = device, dtype
+        self.w: Dict[str, torch.Tensor] = {}
+        self._ws = {}
+
+    # --- weights -----------------------------------------------------------------------------
+    @property
+    def hidden_size(self):
+        return self.E
+
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor]):
+        """Load HF ViTModel / CLIPVisionModel weights (any of the naming schemes above)."""
+        n = {_normalize_hf_key(k): v.detach().float().cpu() for k, v in sd.items()}
+        E, dt, dev = self.E, self.dtype, self.device
+
+        def get(k):
+            if k not in n:
+                raise KeyError(f"encoder weight '{k}' missing (have e.g. {sorted(n)[:4]})")
+            return n[k]
+
+        w = {}
+        if self.kind == "vit":
+            pw = get("embeddings.patch_embeddings.projection.weight").reshape(E, -1)
+            pb = get("embeddings.patch_embeddings.projection.bias")
+            cls = get("embeddings.cls_token").reshape(E)
+            pos = get("embeddings.position_embeddings").reshape(self.N, E)
+        else:
+            pw = get("embeddings.patch_embedding.weight").reshape(E, -1)
+            pb = torch.zeros(E)
+            cls = get("embeddings.class_embedding").reshape(E)
+            pos = get("embeddings.position_embedding.weight").reshape(self.N, E)
+            w["pre_ln.w"] = get("pre_layrnorm.weight")
+            w["pre_ln.b"] = get("pre_layrnorm.bias")
+        pwp = torch.zeros(E, self.kpad)
+        pwp[:, :self.kin] = pw
+        w["patch.w"], w["patch.b"], w["cls"], w["pos"] = pwp, pb, cls, pos
+        for i in range(self.L):
+            p = f"layers.{i}."
+            w[f"{i}.ln1.w"], w[f"{i}.ln1.b"] = get(p + "layernorm_before.weight"), get(p + "layernorm_before.bias")
+            w[f"{i}.ln2.w"], w[f"{i}.ln2.b"] = get(p + "layernorm_after.weight"), get(p + "layernorm_after.bias")
+            w[f"{i}.qkv.w"] = torch.cat([get(p + f"attention.{x}_proj.weight") for x in "qkv"], 0)
+            w[f"{i}.qkv.b"] = torch.cat([get(p + f"attention.{x}_proj.bias") for x in "qkv"], 0)
+            w[f"{i}.o.w"], w[f"{i}.o.b"] = get(p + "attention.o_proj.weight"), get(p + "attention.o_proj.bias")
+            w[f"{i}.fc1.w"], w[f"{i}.fc1.b"] = get(p + "mlp.fc1.weight"), get(p + "mlp.fc1.bias")
+            w[f"{i}.fc2.w"], w[f"{i}.fc2.b"] = get(p + "mlp.fc2.weight"), get(p + "mlp.fc2.bias")
+        if self.kind == "vit":
+            w["final_ln.w"], w["final_ln.b"] = get("layernorm.weight"), get("layernorm.bias")
+        out = {}
+        for k, v in w.items():
+            is_mat = k.endswith(".w") and v.dim() == 2 and not k.endswith("ln.w")
+            out[k] = v.to(device=dev, dtype=dt if is_mat else torch.float32).contiguous()
+        self.w = out
+        return self
+
+    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+        """Weights back in HF transformers-5.x names (ViTModel / CLIPVisionModel), f32 CPU copies."""
+        w, E = {k: v.detach().float().cpu() for k, v in self.w.items()}, self.E
+        sd = {}
+        pw = w["patch.w"][:, :self.kin].reshape(E, 3, self.patch, self.patch).clone()
+        if self.kind == "vit":
+            sd["embeddings.cls_token"] = w["cls"].view(1, 1, E)
+            sd["embeddings.position_embeddings"] = w["pos"].view(1, self.N, E)
+            sd["embeddings.patch_embeddings.projection.weight"] = pw
+            sd["embeddings.patch_embeddings.projection.bias"] = w["patch.b"]
+            lp, att, ln1, ln2 = "layers.", "attention.", "layernorm_before", "layernorm_after"
+            names = dict(q="q_proj", k="k_proj", v="v_proj", o="o_proj")
+        else:
+            sd["embeddings.class_embedding"] = w["cls"]
+            sd["embeddings.patch_embedding.weight"] = pw
+            sd["embeddings.position_embedding.weight"] = w["pos"]
+            sd["pre_layrnorm.weight"], sd["pre_layrnorm.bias"] = w["pre_ln.w"], w["pre_ln.b"]
+            lp, att, ln1, ln2 = "encoder.layers.", "self_attn.", "layer_norm1", "layer_norm2"
+            names = dict(q="q_proj", k="k_proj", v="v_proj", o="out_proj")
+        for i in range(self.L):
+            p = f"{lp}{i}."
+            qw, qb = w[f"{i}.qkv.w"], w[f"{i}.qkv.b"]
+            for j, x in enumerate("qkv"):
+                sd[p + att + names[x] + ".weight"] = qw[j * E:(j + 1) * E].clone()
+                sd[p + att + names[x] + ".bias"] = qb[j * E:(j + 1) * E].clone()
+            sd[p + att + names["o"] + ".weight"], sd[p + att + names["o"] + ".bias"] = w[f"{i}.o.w"], w[f"{i}.o.b"]
+            sd[p + ln1 + ".weight"], sd[p + ln1 + ".bias"] = w[f"{i}.ln1.w"], w[f"{i}.ln1.b"]
+            sd[p + ln2 + ".weight"], sd[p + ln2 + ".bias"] = w[f"{i}.ln2.w"], w[f"{i}.ln2.b"]
+            sd[p + "mlp.fc1.weight"], sd[p + "mlp.fc1.bias"] = w[f"{i}.fc1.w"], w[f"{i}.fc1.b"]
+            sd[p + "mlp.fc2.weight"], sd[p + "mlp.fc2.bias"] = w[f"{i}.fc2.w"], w[f"{i}.fc2.b"]
+        if self.kind == "vit":
+            sd["layernorm.weight"], sd["layernorm.bias"] = w["final_ln.w"], w["final_ln.b"]
+        return sd
+
+    def random_init(self, seed: int = 0):
+        """Seeded random weights in HF naming (no pretrained weights offline)."""
+        g = torch.Generator().manual_seed(seed)
+        E, m = self.E, self.mlp
+
+        def rnd(*s, scale):
+            return torch.randn(*s, generator=g) * scale
+
+        sd = {}
+        if self.kind == "vit":
+            sd["embeddings.patch_embeddings.projection.weight"] = rnd(E, 3, self.patch, self.patch, scale=self.kin ** -0.5)
+            sd["embeddings.patch_embeddings.projection.bias"] = rnd(E, scale=0.02)
+            sd["embeddings.cls_token"] = rnd(1, 1, E, scale=0.02)
+            sd["embeddings.position_embeddings"] = rnd(1, self.N, E, scale=0.02)
+            sd["layernorm.weight"] = 1 + rnd(E, scale=0.02)
+            sd["layernorm.bias"] = rnd(E, scale=0.02)
+        else:
+            sd["embeddings.patch_embedding.weight"] = rnd(E, 3, self.patch, self.patch, scale=self.kin ** -0.5)
+            sd["embeddings.class_embedding"] = rnd(E, scale=0.02)
+            sd["embeddings.position_embedding.weight"] = rnd(self.N, E, scale=0.02)
+            sd["pre_layrnorm.weight"] = 1 + rnd(E, scale=0.02)
+            sd["pre_layrnorm.bias"] = rnd(E, scale=0.02)
+        for i in range(self.L):
+            p = f"layers.{i}."
+            for x in "qkvo":
+                sd[p + f"attention.{x}_proj.weight"] = rnd(E, E, scale=E ** -0.5)
+                sd[p + f"attention.{x}_proj.bias"] = rnd(E, scale=0.02)
+            sd[p + "layernorm_before.weight"] = 1 + rnd(E, scale=0.02)
+            sd[p + "layernorm_before.bias"] = rnd(E, scale=0.02)
+            sd[p + "layernorm_after.weight"] = 1 + rnd(E, scale=0.02)
+            sd[p + "layernorm_after.bias"] = rnd(E, scale=0.02)
+            sd[p + "mlp.fc1.weight"] = rnd(m, E, scale=E ** -0.5)
+            sd[p + "mlp.fc1.bias"] = rnd(m, scale=0.02)
+            sd[p + "mlp.fc2.weight"] = rnd(E, m, scale=m ** -0.5)
+            sd[p + "mlp.fc2.bias"] = rnd(E, scale=0.02)
+        return self.load_hf_state_dict(sd)
+
+    # --- forward -----------------------------------------------------------------------------
+    def _workspace(self, B):
+        if B not in self._ws:
+            R, E, dt, dev = B * self.N, self.E, self.dtype, self.device
+            self._ws[B] = dict(
+                cols=torch.empty(B * self.np, self.kpad, dtype=dt, device=dev),
+                pt=torch.empty(B * self.np, E, dtype=dt, device=dev),
+                h=torch.empty(R, E, dtype=dt, device=dev),
+                a=torch.empty(R, E, dtype=dt, device=dev),
+                qkv=torch.empty(R, 3 * E, dtype=dt, device=dev),
+                o=torch.empty(R, E, dtype=dt, device=dev),
+                m=torch.empty(R, self.mlp, dtype=dt, device=dev),
+                out=torch.empty(R, E, dtype=dt, device=dev),
+            )
+        return self._ws[B]
+
+    def forward(self, images: torch.Tensor, rows: str = "all") -> torch.Tensor:
+        """images f32 [B,3,H,W] (already normalised) -> last_hidden_state in the compute dtype.
+        rows="all": [B, N, E] ; rows="cls": only the CLS rows are finalised, returned as the
+        strided view [B, E] of the [B, N, E] buffer (row stride N*E)."""
+        B = images.shape[0]
+        if tuple(images.shape[1:]) != (3, self.image, self.image):
+            raise ValueError(f"expected images [B,3,{self.image},{self.image}], got {tuple(images.shape)}")
+        images = images.contiguous().float()
+        ws, w, E, N, H = self._workspace(B), self.w, self.E, self.N, self.H
+        R = B * N
+        native.im2col(images, ws["cols"], self.patch, self.kpad)
+        native.linear(ws["cols"], w["patch.w"], ws["pt"], bias=w["patch.b"])
+        h = ws["h"]
+        native.vit_assemble(ws["pt"], w["cls"], w["pos"], h, B, self.np, E)
+        if self.kind == "clip":
+            native.layernorm_fwd(h, w["pre_ln.w"], w["pre_ln.b"], self.eps, ws["a"])
+            h, ws["a"] = ws["a"], h  # swap roles: the normalised tensor is the residual stream
+            ws["h"] = h
+        a, qkv, o, m = ws["a"], ws["qkv"], ws["o"], ws["m"]
+        act = native.ACT_GELU if self.kind == "vit" else native.ACT_QUICK_GELU
+        for i in range(self.L):
+            native.layernorm_fwd(h, w[f"{i}.ln1.w"], w[f"{i}.ln1.b"], self.eps, a)
+            native.linear(a, w[f"{i}.qkv.w"], qkv, bias=w[f"{i}.qkv.b"])
+            args = native.attn_args(qkv, 3 * E, N * 3 * E, qkv[:, E:], 3 * E, N * 3 * E, qkv[:, 2 * E:], 3 * E,
+                                    N * 3 * E, o, E, N * E, scale=1.0 / math.sqrt(64))
+            native.attention_fwd(native.dtype_code(qkv), B, H, N, N, args)
+            native.linear(o, w[f"{i}.o.w"], h, bias=w[f"{i}.o.b"], residual=h)
+            native.layernorm_fwd(h, w[f"{i}.ln2.w"], w[f"{i}.ln2.b"], self.eps, a)
+            native.linear(a, w[f"{i}.fc1.w"], m, bias=w[f"{i}.fc1.b"], act=act)
+            native.linear(m, w[f"{i}.fc2.w"], h, bias=w[f"{i}.fc2.b"], residual=h)
+        if self.kind == "vit":
+            out = ws["out"]
+            if rows == "cls":
+                native.layernorm_fwd(h, w["final_ln.w"], w["final_ln.b"], self.eps, out, rows=B, cols=E, ldx=N * E,
+                                     ldy=N * E)
+                return out.view(B, N, E)[:, 0, :]
+            native.layernorm_fwd(h, w["final_ln.w"], w["final_ln.b"], self.eps, out)
+            return out.view(B, N, E)
+        return h.view(B, N, E)[:, 0, :] if rows == "cls" else h.view(B, N, E)
+
+    def flops_per_image(self) -> float:
+        """Algorithmic forward FLOPs per image (SURVEY.md §8d convention)."""
+        N, E, m = self.N, self.E, self.mlp
+        per_layer = 2 * N * 4 * E * E + 2 * N * 2 * E * m + 4 * N * N * E
+        return self.L * per_layer + 2 * (N - 1) * E * self.kin
+
+
+def get_encoder_output_dim(name: Optional[str] = None) -> int:
+    """encoder.py:112-124 counterpart: hidden size of the named encoder."""
+    return config.ENCODER_SPECS[name or config.ENCODER_MODEL_NAME]["hidden"]
+
+
+def build_encoder(name: Optional[str] = None, device=None, dtype=None, weights_path=None, seed=0) -> VisionEncoder:
+    """model.py:48-66 counterpart without the network: geometry from config.ENCODER_SPECS, weights
+    from a local safetensors file (HF names) if given, else seeded random init."""
+    name = name or config.ENCODER_MODEL_NAME
+    if name not in config.ENCODER_SPECS:
+        raise ValueError(f"encoder '{name}' is not supported (have {sorted(config.ENCODER_SPECS)})")
+    device = device or torch.device("cuda")
+    dtype = dtype or (torch.bfloat16 if config.DTYPE == "bf16" else torch.float32)
+    enc = VisionEncoder(config.ENCODER_SPECS[name], device, dtype)
+    path = weights_path if weights_path is not None else config.ENCODER_WEIGHTS_PATH
+    if path:
+        from safetensors.torch import load_file
+        enc.load_hf_state_dict(load_file(path))
+    else:
+        enc.random_init(seed)
+    return enc

@@ -1,0 +1,273 @@
+"""ImageToTextModel: frozen vision encoder + projection + Transformer decoder (reference model.py:12-255).
+
+Drop-in surface:
+  * ``ImageToTextModel(decoder_vocab_size, decoder_embed_dim, decoder_heads, decoder_layers,
+    decoder_ff_dim, decoder_max_seq_len, decoder_dropout, decoder_pad_idx)`` (model.py:14-16), the
+    encoder chosen by config.ENCODER_MODEL_NAME;
+  * ``forward(image_tensors f32[B,3,H,W], tgt_tokens i64[B,T]) -> f32[B,T,V]`` (model.py:116-169);
+  * ``generate(image, start_token_id, end_token_id, max_len=100, method='greedy', beam_size=3)``
+    (model.py:171-255);
+  * ``state_dict()`` / ``load_state_dict()`` in the reference's key names.
+Added for the MI355X path:
+  * ``train_step(images, decoder_input_tokens, target_tokens, dist=None)``: the whole of
+    train.py:75-93 (forward, CE(ignore PAD), backward) as one kernel sequence with no host sync,
+    returning the loss as a device scalar; ``optim.AdamW.step(clip)`` finishes train.py:96-100.
+  * ``memory_mode`` "cls" (reference: CLS token only, model.py:141) or "patches" (north star:
+    cross-attention over the projected patch sequence).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+import config
+import native
+from decoder import TransformerDecoder, decoder_entries, flat_to_reference, reference_to_flat
+from encoder import VisionEncoder, build_encoder
+from params import FlatParams
+
+
+def _dtype_from_config(dtype):
+    if dtype is None:
+        dtype = config.DTYPE
+    if isinstance(dtype, torch.dtype):
+        return dtype
+    return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32}[dtype]
+
+
+class ViTImageProcessorLite:
+    """ViTImageProcessor defaults (tf/models/vit/image_processing_vit.py; mean = std = 0.5,
+    tf/utils/constants.py:3-4): RGB, resize to size x size with PIL bilinear, /255, (x - 0.5)/0.5.
+    Host-side preprocessing, used by generate() (model.py:192)."""
+
+    def __init__(self, size: int = 224, mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5)):
+        self.size, self.mean, self.std = size, np.asarray(mean, np.float32), np.asarray(std, np.float32)
+
+    def __call__(self, images, return_tensors="pt"):
+        from PIL import Image
+        ims = images if isinstance(images, (list, tuple)) else [images]
+        out = []
+        for im in ims:
+            if not isinstance(im, Image.Image):
+                im = Image.fromarray(np.asarray(im))
+            im = im.convert("RGB").resize((self.size, self.size), Image.BILINEAR)
+            a = np.asarray(im, dtype=np.float32) / 255.0
+            a = (a - self.mean) / self.std
+            out.append(torch.from_numpy(a.transpose(2, 0, 1).copy()))
+        return {"pixel_values": torch.stack(out)}
+
+
+class ImageToTextModel:
+    def __init__(self, decoder_vocab_size: int, decoder_embed_dim: int, decoder_heads: int, decoder_layers: int,
+                 decoder_ff_dim: int, decoder_max_seq_len: int, decoder_dropout: float, decoder_pad_idx: int, *,
+                 encoder: Optional[VisionEncoder] = None, memory_mode: Optional[str] = None, dtype=None, device=None,
+                 seed: Optional[int] = None):
+        native.require_gpu()
+        native.load_library()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.dtype = _dtype_from_config(dtype)
+        seed = config.RANDOM_SEED if seed is None else seed
+        self.encoder = encoder if encoder is not None else build_encoder(device=self.device, dtype=self.dtype,
+                                                                          seed=seed)
+        if self.encoder.dtype != self.dtype:
+            raise ValueError("encoder and model compute dtypes differ")
+        self.memory_mode = memory_mode or config.MEMORY_MODE
+        if self.memory_mode not in ("cls", "patches"):
+            raise ValueError(f"memory_mode must be 'cls' or 'patches', got {self.memory_mode}")
+        self.encoder_output_dim = self.encoder.hidden_size
+        self.decoder_embed_dim = decoder_embed_dim
+        self.decoder_pad_idx = decoder_pad_idx
+        E, d = self.encoder_output_dim, decoder_embed_dim
+        self.has_projection = E != d  # model.py:97-102: Linear if dims differ, else Identity
+        self.store = FlatParams(decoder_entries(decoder_vocab_size, d, decoder_layers, decoder_ff_dim,
+                                                E if self.has_projection else None), self.device, self.dtype)
+        self.decoder = TransformerDecoder(decoder_vocab_size, d, decoder_heads, decoder_layers, decoder_ff_dim,
+                                          decoder_max_seq_len, decoder_dropout, decoder_pad_idx, store=self.store,
+                                          device=self.device)
+        self.decoder.init_weights(seed + 1)
+        if self.has_projection:
+            g = torch.Generator().manual_seed(seed + 2)
+            b = 1.0 / math.sqrt(E)  # nn.Linear default init bounds
+            self.store.p("projection.weight").copy_((torch.rand(d, E, generator=g) * 2 - 1) * b)
+            self.store.p("projection.bias").copy_((torch.rand(d, generator=g) * 2 - 1) * b)
+            self.store.sync_shadow()
+        self.image_processor = ViTImageProcessorLite(self.encoder.image)
+        self.training = True
+        # dropout RNG state: a device counter (graph-replay safe), distinct per DP rank
+        self.seed_t = torch.tensor([seed * 1000003], dtype=torch.int64, device=self.device)
+        self._mem: Dict[tuple, torch.Tensor] = {}
+
+    # --- nn.Module-like surface ----------------------------------------------------------------
+    def train(self, mode: bool = True):
+        self.training = mode
+        self.decoder.train(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def to(self, device):
+        if torch.device(device).type != self.device.type:
+            raise ValueError("ImageToTextModel lives on the GPU it was built on")
+        return self
+
+    def parameters(self):
+        return [self.store.master]
+
+    def num_trainable(self) -> int:
+        return sum(n for _, _, _, n in self.store.entries)
+
+    def set_rank_seed(self, rank: int, seed: Optional[int] = None):
+        """Dropout streams differ per data-parallel rank."""
+        seed = config.RANDOM_SEED if seed is None else seed
+        self.seed_t.fill_(seed * 1000003 + rank * 7919 * 65537)
+
+    # --- memory (encoder -> projection) ----------------------------------------------------------
+    def _encode_memory(self, images: torch.Tensor):
+        """Returns (mem_rows, mem_ld, S, enc_rows, enc_ld): memory [B*S rows of d] and the
+        encoder features that feed the projection (for its weight gradient)."""
+        B = images.shape[0]
+        N, E, d = self.encoder.N, self.encoder.E, self.decoder_embed_dim
+        if self.memory_mode == "cls":
+            enc = self.encoder.forward(images, rows="cls")  # [B, E] view, row stride N*E
+            S, enc_rows, enc_ld = 1, enc, N * E
+        else:
+            enc = self.encoder.forward(images, rows="all")  # [B, N, E]
+            S, enc_rows, enc_ld = N, enc.reshape(B * N, E), E
+        if not self.has_projection:
+            return enc_rows, enc_ld, S, enc_rows, enc_ld
+        key = (B, S)
+        if key not in self._mem:
+            self._mem[key] = torch.empty(B * S, d, dtype=self.dtype, device=self.device)
+        mem = self._mem[key]
+        native.gemm(enc_rows, self.store.w("projection.weight"), mem, B * S, d, E, lda=enc_ld,
+                    bias=self.store.p("projection.bias"))
+        return mem, d, S, enc_rows, enc_ld
+
+    # --- forward (model.py:116-169) ------------------------------------------------------------
+    def forward(self, image_tensors: torch.Tensor, tgt_tokens: torch.Tensor) -> torch.Tensor:
+        images = image_tensors.to(self.device)
+        tokens = tgt_tokens.to(self.device, torch.int64).contiguous()
+        B, T = tokens.shape
+        mem, mem_ld, S, _, _ = self._encode_memory(images)
+        A = self.decoder.acts(B, T, S, False)
+        out = torch.empty(B * T, self.decoder.V, dtype=torch.float32, device=self.device)
+        p = self.decoder.dropout if self.training else 0.0
+        if p > 0:
+            native.step_inc(self.seed_t)
+        self.decoder.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, False, logits_out=out, drop_p=p)
+        return out.view(B, T, self.decoder.V)
+
+    __call__ = forward
+
+    # --- fused train step (train.py:75-93) -----------------------------------------------------
+    def train_step(self, images: torch.Tensor, decoder_input_tokens: torch.Tensor, target_tokens: torch.Tensor,
+                   dist=None) -> torch.Tensor:
+        """Forward + CE(ignore PAD, mean over the GLOBAL non-PAD count) + backward into the flat
+        gradient buffer. Returns the loss as a device scalar [1] (no host sync)."""
+        images = images.to(self.device, non_blocking=True)
+        tokens = decoder_input_tokens.to(self.device, torch.int64, non_blocking=True).contiguous()
+        targets = target_tokens.to(self.device, torch.int64, non_blocking=True).contiguous()
+        B, T = tokens.shape
+        mem, mem_ld, S, enc_rows, enc_ld = self._encode_memory(images)
+        dec = self.decoder
+        A = dec.acts(B, T, S, True)
+        native.step_inc(self.seed_t)
+        logits, _ = dec.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, True)
+        native.zero(A.count)
+        native.zero(A.loss_sum)
+        native.count_targets(targets, self.decoder_pad_idx, A.count)
+        if dist is not None:
+            dist.all_reduce_count(A.count)
+        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, True)
+        proj = (enc_rows, enc_ld, self.encoder_output_dim) if self.has_projection else None
+        dec.run_backward(tokens, mem, mem_ld, S, A, self.seed_t, logits, proj_input=proj,
+                         grads_ready=dist.grads_ready if dist is not None else None)
+        native.scalar_div(A.loss_sum, A.count, A.loss)
+        if dist is not None:
+            dist.finish_backward(A.loss)
+        return A.loss
+
+    @torch.no_grad()
+    def eval_loss(self, images, decoder_input_tokens, target_tokens) -> torch.Tensor:
+        """train.py:141-145 (forward + CE) without materialising f32 logits; device scalar."""
+        images = images.to(self.device)
+        tokens = decoder_input_tokens.to(self.device, torch.int64).contiguous()
+        targets = target_tokens.to(self.device, torch.int64).contiguous()
+        B, T = tokens.shape
+        mem, mem_ld, S, _, _ = self._encode_memory(images)
+        A = self.decoder.acts(B, T, S, False)
+        logits, _ = self.decoder.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, False, drop_p=0.0)
+        native.zero(A.count)
+        native.zero(A.loss_sum)
+        native.count_targets(targets, self.decoder_pad_idx, A.count)
+        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, False)
+        native.scalar_div(A.loss_sum, A.count, A.loss)
+        return A.loss
+
+    # --- generate (model.py:171-255) -----------------------------------------------------------
+    @torch.no_grad()
+    def generate(self, image, start_token_id, end_token_id, max_len=100, method="greedy", beam_size=3) -> List[int]:
+        if method == "beam":
+            print("Beam search not fully implemented in this example. Falling back to greedy.")
+            method = "greedy"
+        if method != "greedy":
+            raise ValueError(f"Unsupported generation method: {method}. Choose 'greedy' or 'beam'.")
+        self.eval()
+        if isinstance(image, torch.Tensor):
+            pv = image if image.dim() == 4 else image.unsqueeze(0)
+        else:
+            pv = self.image_processor(images=image, return_tensors="pt")["pixel_values"]
+        pv = pv.to(self.device).float()
+        mem, mem_ld, S, _, _ = self._encode_memory(pv)
+        mem3 = mem.view(1, S, -1) if mem_ld == self.decoder_embed_dim else None
+        if mem3 is None:  # identity projection + cls: gather the strided row
+            mem3 = mem[:1].reshape(1, 1, -1).contiguous()
+        ids = [int(start_token_id)]
+        for _ in range(max_len - 1):
+            logits = self.decoder.forward(torch.tensor([ids], device=self.device), mem3)
+            nxt = int(torch.argmax(logits[0, -1]).item())
+            ids.append(nxt)
+            if nxt == end_token_id:
+                break
+        return ids
+
+    # --- checkpoints (reference key names) --------------------------------------
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        sd = {}
+        for k, v in self.encoder.hf_state_dict().items():
+            sd["encoder." + k] = v
+        if self.has_projection:
+            sd["projection.weight"] = self.store.p("projection.weight").detach().clone()
+            sd["projection.bias"] = self.store.p("projection.bias").detach().clone()
+        sd.update(flat_to_reference(self.store, self.decoder.L, self.decoder_embed_dim))
+        sd["decoder.positional_encoding.pe"] = self.decoder.pe.unsqueeze(0).clone()
+        return sd
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        enc = {k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")}
+        if enc:
+            self.encoder.load_hf_state_dict(enc)
+        flat = reference_to_flat(sd, self.decoder.L, self.decoder_embed_dim)
+        names = set(self.store.names())
+        missing = sorted(names - set(flat))
+        if strict and missing:
+            raise KeyError(f"missing keys for: {missing[:6]}{'...' if len(missing) > 6 else ''}")
+        with torch.no_grad():
+            for k, v in flat.items():
+                if k in names:
+                    self.store.p(k).copy_(v.to(self.device, torch.float32).reshape(self.store.p(k).shape))
+        self.store.sync_shadow()
+        return self
+
+    # --- accounting ----------------------------------------------------------------------------
+    def flops_per_pair(self, T: int) -> float:
+        """Algorithmic train FLOPs per image-caption pair: encoder fwd + 3 x decoder fwd
+        (+ the projection, counted with the decoder as 3 x its forward)."""
+        S = 1 if self.memory_mode == "cls" else self.encoder.N
+        dec = self.decoder.flops_per_sequence(T, S)
+        proj = 2 * S * self.encoder.E * self.decoder_embed_dim if self.has_projection else 0
+        return self.encoder.flops_per_image() + 3 * (dec + proj)

@@ -80,6 +80,8 @@ SIGNATURES = {
     "mit_step_inc": (I, [vp, vp]),
     "mit_adamw": (I, [L, vp, vp, vp, vp, vp, vp, vp, vp, Fl, Fl, Fl, Fl, vp]),
     "mit_cast_f32": (I, [I, L, vp, vp, vp]),
+    "mit_zero": (I, [vp, L, vp]),
+    "mit_scalar_div": (I, [vp, vp, vp, vp]),
     "mit_dropout_mask": (I, [L, Fl, vp, U32, vp, vp]),
 }
 
@@ -236,12 +238,22 @@ def count_targets(targets, ignore_index, count):
            "mit_count_targets")
 
 
-def cross_entropy(logits, targets, ignore_index, grad_scale, loss_sum, want_grad, rows=None, V=None, ld=None):
+def cross_entropy(logits, targets, ignore_index, count, loss_sum, want_grad, rows=None, V=None, ld=None):
+    """loss_sum += sum of -log p[target]; if want_grad, logits <- (softmax - onehot) / count (in place)."""
     V = V if V is not None else logits.shape[-1]
     rows = rows if rows is not None else targets.numel()
     _check(lib().mit_cross_entropy(dtype_code(logits), rows, V, ptr(logits), ld or V, ptr(targets), ignore_index,
-                                   ptr(grad_scale), ptr(loss_sum), 1 if want_grad else 0, stream_ptr()),
+                                   ptr(count), ptr(loss_sum), 1 if want_grad else 0, stream_ptr()),
            "mit_cross_entropy")
+
+
+def scalar_div(a, b, out):
+    _check(lib().mit_scalar_div(ptr(a), ptr(b), ptr(out), stream_ptr()), "mit_scalar_div")
+
+
+def zero(t):
+    """Zero a tensor's storage span with hipMemsetAsync (t must be contiguous)."""
+    _check(lib().mit_zero(ptr(t), t.numel() * t.element_size(), stream_ptr()), "mit_zero")
 
 
 def colsum_ws_floats(M, N):

@@ -1,0 +1,79 @@
+"""Flat parameter storage: ONE f32 master buffer, ONE f32 gradient buffer, the AdamW moments, and a
+bf16 shadow copy the GEMMs read (bf16 mode). Named tensors are views into these buffers.
+
+Entries are laid out in the order the backward FINISHES them (fc_out first, then decoder layers
+top-down, the fused cross-attention K/V block, the embedding, the projection), so a data-parallel
+gradient all-reduce can launch contiguous buckets while the rest of the backward still runs.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+
+import native
+
+ALIGN = 64  # elements: keeps every view 256-B aligned for 16-B vector access in every dtype
+
+
+class FlatParams:
+    def __init__(self, entries: Sequence[Tuple[str, Tuple[int, ...]]], device, compute_dtype: torch.dtype):
+        self.entries: List[Tuple[str, Tuple[int, ...], int, int]] = []
+        off = 0
+        for name, shape in entries:
+            n = 1
+            for s in shape:
+                n *= s
+            self.entries.append((name, tuple(shape), off, n))
+            off += (n + ALIGN - 1) // ALIGN * ALIGN
+        self.numel = off
+        self.index: Dict[str, Tuple[Tuple[int, ...], int, int]] = {e[0]: (e[1], e[2], e[3]) for e in self.entries}
+        self.device = device
+        self.compute_dtype = compute_dtype
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        if compute_dtype == torch.float32:
+            self.shadow = self.master
+        else:
+            self.shadow = torch.zeros(self.numel, dtype=compute_dtype, device=device)
+        self.exp_avg = None
+        self.exp_avg_sq = None
+
+    # views ------------------------------------------------------------------------------------
+    def _view(self, buf, name):
+        shape, off, n = self.index[name]
+        return buf[off:off + n].view(shape)
+
+    def p(self, name):
+        """f32 master view."""
+        return self._view(self.master, name)
+
+    def w(self, name):
+        """compute-dtype view (what kernels read)."""
+        return self._view(self.shadow, name)
+
+    def g(self, name):
+        return self._view(self.grad, name)
+
+    def span(self, first: str, last: str):
+        """[start, end) element range covering entries first..last (inclusive, layout order)."""
+        s = self.index[first][1]
+        _, off, n = self.index[last]
+        return s, off + n
+
+    def names(self):
+        return [e[0] for e in self.entries]
+
+    # maintenance ------------------------------------------------------------------------------
+    def sync_shadow(self):
+        """master -> bf16 shadow (after a load / manual edit; AdamW keeps them in sync itself)."""
+        if self.shadow is not self.master:
+            native.cast_f32(self.master, self.shadow)
+
+    def zero_grad(self):
+        native.zero(self.grad)
+
+    def ensure_optimizer_state(self):
+        if self.exp_avg is None:
+            self.exp_avg = torch.zeros_like(self.master)
+            self.exp_avg_sq = torch.zeros_like(self.master)

@@ -1,0 +1,65 @@
+"""Host-side logic that needs no GPU: HF key normalisation, reference <-> flat state-dict mapping,
+flat-buffer layout, FLOP accounting."""
+import pytest
+import torch
+
+import fixtures as FX
+
+
+def test_hf_key_normalisation_vit5_vit4_clip():
+    from encoder import _normalize_hf_key as n
+    # transformers 5.x ViT (as the fixtures / reference state_dict carry them, with 'encoder.' prefix)
+    assert n("encoder.layers.3.attention.q_proj.weight") == "layers.3.attention.q_proj.weight"
+    assert n("encoder.layernorm.weight") == "layernorm.weight"
+    assert n("encoder.embeddings.cls_token") == "embeddings.cls_token"
+    assert n("layers.0.mlp.fc1.bias") == "layers.0.mlp.fc1.bias"
+    # transformers 4.x ViT: ViTModel keys ('encoder.layer.N...') with and without the model prefix
+    assert n("encoder.layer.2.attention.attention.query.weight") == "layers.2.attention.q_proj.weight"
+    assert n("encoder.encoder.layer.2.attention.output.dense.bias") == "layers.2.attention.o_proj.bias"
+    assert n("encoder.layer.5.intermediate.dense.weight") == "layers.5.mlp.fc1.weight"
+    assert n("encoder.layer.5.output.dense.weight") == "layers.5.mlp.fc2.weight"
+    assert n("encoder.layer.5.layernorm_before.weight") == "layers.5.layernorm_before.weight"
+    # CLIP vision (5.x CLIPVisionModel and CLIPModel.vision_model)
+    assert n("encoder.encoder.layers.1.self_attn.out_proj.weight") == "layers.1.attention.o_proj.weight"
+    assert n("vision_model.encoder.layers.1.layer_norm2.bias") == "layers.1.layernorm_after.bias"
+    assert n("encoder.pre_layrnorm.weight") == "pre_layrnorm.weight"
+
+
+@pytest.mark.parametrize("name", ["tiny_vit_cls", "cfg1_b2_patches"])
+def test_reference_flat_roundtrip(name):
+    """reference_to_flat / flat_to_reference are inverse on the fixture weights (CPU FlatParams)."""
+    from decoder import decoder_entries, flat_to_reference, reference_to_flat
+    from params import FlatParams
+    meta, _ = FX.load(name)
+    st = FX.state(meta)
+    dec = FX.dec_desc(meta)
+    E = FX.enc_desc(meta)["hidden"]
+    store = FlatParams(decoder_entries(dec["vocab"], dec["d"], dec["layers"], dec["ff"],
+                                       E if E != dec["d"] else None), torch.device("cpu"), torch.float32)
+    flat = reference_to_flat({k: v for k, v in st.items() if not k.startswith("encoder.")}, dec["layers"], dec["d"])
+    assert set(flat) == set(store.names())
+    for k, v in flat.items():
+        store.p(k).copy_(v)
+    back = flat_to_reference(store, dec["layers"], dec["d"])
+    for k, v in back.items():
+        torch.testing.assert_close(v, st[k], rtol=0, atol=0)
+    # layout: 256-B aligned views, ordered fc_out first, embedding/projection last
+    for _, _, off, _ in store.entries:
+        assert off % 64 == 0
+    assert store.names()[0] == "fc_out.weight"
+
+
+def test_cfg1_flop_accounting_matches_survey():
+    """cfg1 patches 50.17 GFLOP/pair, cls 45.56."""
+    import math
+    from decoder import decoder_entries
+    N, E, mlp, Lenc = 197, 768, 3072, 12
+    enc = Lenc * (2 * N * 4 * E * E + 2 * N * 2 * E * mlp + 4 * N * N * E) + 2 * (N - 1) * E * 768
+    T, d, F, V, L = 63, 512, 2048, 10000, 6
+
+    def dec(S):
+        layer = 2 * T * 3 * d * d + 2 * T * d * d + 4 * T * T * d + 2 * T * d * d + 2 * S * 2 * d * d \
+            + 4 * T * S * d + 2 * T * d * d + 2 * T * 2 * d * F
+        return L * layer + 2 * T * d * V + 2 * S * E * d
+    assert abs((enc + 3 * dec(197)) / 1e9 - 50.17) < 0.05
+    assert abs((enc + 3 * dec(1)) / 1e9 - 45.56) < 0.05

@@ -247,13 +247,15 @@ def test_embed_ce_colsum(dtype):
     cnt = torch.zeros(1, device=dev())
     N.count_targets(tgt, 0, cnt)
     assert cnt.item() == (tgt != 0).sum().item()
-    gs = 1.0 / cnt
     ls = torch.zeros(1, device=dev())
     lr = logits.float().clone().requires_grad_(True)
     ref = F.cross_entropy(lr, tgt, ignore_index=0)
     ref.backward()
     g = logits.clone()
-    N.cross_entropy(g, tgt, 0, gs, ls, True)
+    N.cross_entropy(g, tgt, 0, cnt, ls, True)
+    mean = torch.empty(1, device=dev())
+    N.scalar_div(ls, cnt, mean)
+    assert abs(mean.item() - ref.item()) < 1e-4 * abs(ref.item()) + 1e-5
     assert abs(ls.item() / cnt.item() - ref.item()) < 1e-4 * abs(ref.item()) + 1e-5
     _close(g, lr.grad, 1e-2 if dtype == torch.bfloat16 else 1e-5)
     # colsum
