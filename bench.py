@@ -1,0 +1,216 @@
+"""Throughput benchmark of the MI355X train step (BASELINE.json metric: image-caption pairs/sec).
+
+Workload (BASELINE.json configs[1]): 6-layer d_model=512 decoder + ViT-B/16 encoder (197 patches,
+memory_mode "patches": the decoder cross-attends to the projected patch sequence), bf16 compute
+with f32 master weights / grads / AdamW state, batch 64 per GPU, 64-token captions (decoder T=63),
+vocab 10000, dropout 0.1, synthetic data (randn images, random caption ids), random-init weights.
+One step = encoder forward + projection + decoder forward + CE + backward + clip_grad_norm_(5.0)
++ AdamW, i.e. train.py:75-100 for one batch.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL data parallel)
+
+Rank 0 prints ONE JSON line. `value` = pairs processed by all ranks / max-over-ranks wall time.
+`roofline` = the dominant kernel's achieved algorithmic TFLOP/s (HIP events around each of its
+launches during an instrumented replay of the same steps) against the bf16 dense MFMA peak.
+`cpu_baseline` = the CPU oracle (oracle/ref_cpu.py, an fp32 PyTorch restatement of the reference
+path) timed on this host on a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "multimodal-image-transformer_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+MFMA_BF16_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
+METRIC = "image-caption pairs/sec (train step), 6L/d512 decoder + ViT-B/16, 1/2/4/8 GPU"
+
+
+class GemmProbe:
+    """HIP events around every GEMM launch, grouped by kernel instance (a_layout, b_layout)."""
+
+    def __init__(self):
+        self.rec = []
+        self.cur = None
+
+    def before(self, dt, al, bl, M, N, K):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.cur = (e0, (al, bl), 2.0 * M * N * K)
+
+    def after(self):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        e0, key, fl = self.cur
+        self.rec.append((e0, e1, key, fl))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for e0, e1, key, fl in self.rec:
+            t = e0.elapsed_time(e1) * 1e-3
+            a = agg.setdefault(key, [0.0, 0.0, 0])
+            a[0] += t
+            a[1] += fl
+            a[2] += 1
+        return agg
+
+
+def build(args, rank):
+    import config
+    from model import ImageToTextModel
+    import optim
+    config.MEMORY_MODE = args.memory_mode
+    m = ImageToTextModel(args.vocab, 512, 8, 6, 2048, 100, 0.1, 0, memory_mode=args.memory_mode, dtype=args.dtype,
+                         seed=42)
+    opt = optim.AdamW(m.store, lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-5)
+    return m, opt
+
+
+def synthetic_batch(B, seq_len, vocab, device, seed):
+    g = torch.Generator().manual_seed(seed)
+    images = torch.randn(B, 3, 224, 224, generator=g).to(device)
+    cap = torch.randint(4, vocab, (B, seq_len), generator=g)
+    cap[:, 0] = 2
+    return images, cap[:, :-1].contiguous().to(device), cap[:, 1:].contiguous().to(device)
+
+
+def cpu_baseline(model, args):
+    """The CPU oracle's train step (fp32, torch CPU, dropout off) on a bounded sample of the same
+    workload: cfg1 architecture, patches mode, `cpu_batch` pairs per step, same weights."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle import ref_cpu as R
+    sd = {k: v.float().cpu() for k, v in model.state_dict().items()}
+    names = [k for k in sd if not k.startswith("encoder.") and not k.endswith("positional_encoding.pe")]
+    enc = {"kind": "vit", "heads": 12, "layers": 12, "patch": 16, "eps": 1e-12}
+    dec = {"heads": 8, "layers": 6, "max_seq_len": 100}
+    B = args.cpu_batch
+    images, di, tg = synthetic_batch(B, args.seq_len, args.vocab, "cpu", 7)
+    opt = R.AdamWState({k: sd[k] for k in names})
+    R.train_step(sd, names, opt, images, di, tg, enc, dec, args.memory_mode, 5.0)  # warm-up
+    times = []
+    for _ in range(args.cpu_steps):
+        t0 = time.perf_counter()
+        R.train_step(sd, names, opt, images, di, tg, enc, dec, args.memory_mode, 5.0)
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    med = times[len(times) // 2]
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": B / med, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/ref_cpu.py fp32 train step, cfg1 architecture ({args.memory_mode}), batch {B}, "
+                      f"median of {args.cpu_steps} steps after 1 warm-up, dropout off; cpu: {cpu_model}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="pairs per GPU")
+    ap.add_argument("--seq-len", type=int, default=64)
+    ap.add_argument("--vocab", type=int, default=10000)
+    ap.add_argument("--memory-mode", default="patches", choices=["patches", "cls"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true")
+    args = ap.parse_args()
+
+    from dist import DataParallel, init_from_env
+    import torch.distributed as tdist
+    rank, world = init_from_env()
+    if world == 1:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    model, opt = build(args, rank)
+    dp = DataParallel(model, overlap=not args.no_overlap) if world > 1 else None
+    model.train()
+    images, di, tg = synthetic_batch(args.batch, args.seq_len, args.vocab, dev, 1000 + rank)
+
+    def step():
+        model.train_step(images, di, tg, dist=dp)
+        opt.step(5.0)
+
+    def barrier():
+        if world > 1:
+            tdist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss = model.train_step(images, di, tg, dist=dp).item()
+
+    pairs = args.batch * world * args.steps
+    value = pairs / elapsed
+    flops_pair = model.flops_per_pair(args.seq_len - 1)
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.dtype == "bf16" else "f32",
+        "data": "synthetic (randn 224x224 images, uniform caption ids; random-init weights)",
+        "config": {"workload": "configs[1]: 6L d512 decoder + ViT-B/16 (197 patches), batch 64/GPU, seq_len 64",
+                   "global_batch": args.batch * world, "seq_len": args.seq_len, "vocab": args.vocab,
+                   "memory_mode": args.memory_mode, "parallelism": f"dp{world}",
+                   "gflop_per_pair": round(flops_pair / 1e9, 3)},
+        "step_mfma_frac": round(value / world * flops_pair / (MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+        "final_loss": round(loss, 4),
+    }
+    if not args.no_roofline:
+        import native
+        probe = GemmProbe()
+        native.set_gemm_probe(probe)
+        for _ in range(min(args.steps, 5)):
+            step()
+        native.set_gemm_probe(None)
+        agg = probe.summary()
+        names = {(0, 0): "gemm_bf16_kernel<0,0> (NT: forward)", (0, 1): "gemm_bf16_kernel<0,1> (NN: dX)",
+                 (1, 1): "gemm_bf16_kernel<1,1> (TN: dW)", (1, 0): "gemm_bf16_kernel<1,0>"}
+        key = max(agg, key=lambda k: agg[k][0])
+        t, fl, n = agg[key]
+        ach = fl / t / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": names.get(key, str(key)), "achieved": round(ach, 1),
+                           "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
+                           "traffic": None, "launches": n, "avg_launch_us": round(1e6 * t / n, 2)}
+        out["gemm_breakdown"] = {names.get(k, str(k)): {"tflops": round(v[1] / v[0] / 1e12, 1),
+                                                        "ms_per_step": round(1e3 * v[0] / min(args.steps, 5), 3)}
+                                 for k, v in agg.items()}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(model, args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -12,6 +12,8 @@
 //     Used for fp32 parity mode and for the decoder backward.
 //   * attn_fwd_mfma (bf16): 64-query block per 4-wave workgroup, v_mfma_f32_16x16x32_bf16 for
 //     Q K^T and P V with online softmax over 64-key tiles staged in LDS.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -269,6 +271,178 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_simple(long H, long Lq, long 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16 MFMA forward. Workgroup = 4 waves x 16 queries of one (b, h); 64-key K/V tiles, LDS double
+// buffer filled by buffer loads (rows past Lk read as zero, then masked).
+//   S^T = K Q^T  (A = K tile rows from LDS via ds_read_b128, B = Q fragment held in registers):
+//     lane l owns query q = l&15 and keys 16nb + 4(l>>4) + t  -> row softmax = 16 in-lane values
+//     + two cross-lane shuffles (xor 16, 32); online max/sum in log2 units.
+//   O^T = V^T P^T (A = V^T via ds_read_b64_tr_b16 from the row-major V tile, B = P^T straight
+//     from the S^T accumulators, k index permuted consistently: element j<4 -> key 32kk+4g+j,
+//     j>=4 -> key 32kk+16+4g+j-4), so P never touches LDS.
+// ------------------------------------------------------------------------------------------------
+constexpr int AQ = 64;  // queries per workgroup
+constexpr int AK = 64;  // keys per tile
+constexpr uint32_t A_OOB = 0x80000000u;
+
+__device__ __forceinline__ int koff_k(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+__device__ __forceinline__ int koff_v(int r, int byte) { return r * 128 + (byte ^ (((r >> 1) & 3) << 5)); }
+
+__global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, AttnK a, int kbytes, int vbytes) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 2 * AK * D * 2];  // 2 stages x (K, V) x 8 KiB
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const long b = blockIdx.z, h = blockIdx.y;
+  const long qblk = (long)blockIdx.x * AQ;
+  const long qi = qblk + w * 16 + (lane & 15);
+  const bool qlive = qi < Lq;
+  const bf16* Kb = (const bf16*)a.k + b * a.k_batch + h * D;
+  const bf16* Vb = (const bf16*)a.v + b * a.v_batch + h * D;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, kbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, vbytes, 0x00020000);
+  // Q fragments (B operand): Q[qi][32kk + 8g .. +8]
+  bf16x8 qf[2];
+  {
+    const bf16* Qr = (const bf16*)a.q + b * a.q_batch + h * D + (qlive ? qi : 0) * a.q_row;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 v = *(const u32x4*)(Qr + kk * 32 + g * 8);
+      if (!qlive) v = u32x4{0u, 0u, 0u, 0u};
+      qf[kk] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  const float sl2 = a.scale * 1.4426950408889634f;  // scores in log2 units
+  const uint64_t key = a.dropout ? site_key(a.seed, a.site) : 0ull;
+  const uint64_t rowbase = ((uint64_t)(b * H + h) * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
+  const int64_t* tok = a.tok ? a.tok + b * a.tok_batch : nullptr;
+
+  long kend = Lk;
+  if (a.causal) kend = min(Lk, min(Lq, qblk + AQ));  // keys beyond the block's last query are masked
+  const int nt = (int)((kend + AK - 1) / AK);
+
+  u32x4 kr[2], vr[2];
+  auto gload = [&](long j0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 256 * i, r = id >> 3, c = id & 7;
+      const long kj = j0 + r;
+      const bool ok = kj < Lk;
+      kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rk, (int)(ok ? (uint32_t)((kj * a.k_row + c * 8) * 2) : A_OOB), 0, 0));
+      vr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rv, (int)(ok ? (uint32_t)((kj * a.v_row + c * 8) * 2) : A_OOB), 0, 0));
+    }
+  };
+  auto lstore = [&](int s) {
+    char* Ks = lds + s * (2 * AK * D * 2);
+    char* Vs = Ks + AK * D * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 256 * i, r = id >> 3, c = id & 7;
+      *(u32x4*)(Ks + koff_k(r, c)) = kr[i];
+      *(u32x4*)(Vs + koff_v(r, c * 16)) = vr[i];
+    }
+  };
+
+  f32x4 ot[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  if (nt > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nt; ++it) {
+    const int cur = it & 1;
+    const long j0 = (long)it * AK;
+    const bool more = it + 1 < nt;
+    if (more) gload(j0 + AK);
+    const char* Ks = lds + cur * (2 * AK * D * 2);
+    const char* Vs = Ks + AK * D * 2;
+    // ---- S^T = K Q^T ----
+    f32x4 st[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) st[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const u32x4 kv = *(const u32x4*)(Ks + koff_k(nb * 16 + (lane & 15), kk * 4 + g));
+        st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv), qf[kk], st[nb], 0, 0, 0);
+      }
+    // ---- mask + online softmax (per query = per lane&15) ----
+    float s[16];
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const long kj = j0 + nb * 16 + g * 4 + t;
+        bool msk = kj >= Lk || (a.causal && kj > qi);
+        if (!msk && tok) msk = tok[kj] == a.pad;
+        const float v = msk ? -INFINITY : st[nb][t] * sl2;
+        s[nb * 4 + t] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(m, tmax);
+    const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m - mnew);
+    float psum = 0.f;
+    float p[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      p[k] = (s[k] == -INFINITY) ? 0.f : exp2f(s[k] - mnew);
+      psum += p[k];
+    }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    l = l * alpha + psum;
+    m = mnew;
+    if (a.dropout) {
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          p[nb * 4 + t] *= drop_mul(key, rowbase + (uint64_t)(j0 + nb * 16 + g * 4 + t), a.thresh, a.dscale);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ot[i] *= alpha;
+    // ---- O^T += V^T P^T ----
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (bf16)p[(2 * kk) * 4 + j];
+        pb[4 + j] = (bf16)p[(2 * kk + 1) * 4 + j];
+      }
+      const int q = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int colb = (i * 16 + 4 * pp) * 2;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vs + koff_v(kk * 32 + g * 4 + q, colb)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vs + koff_v(kk * 32 + 16 + g * 4 + q, colb)));
+        s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        ot[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pb, ot[i], 0, 0, 0);
+      }
+    }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (!qlive) return;
+  const float inv = 1.0f / l;  // fully masked row: 0 * inf = NaN, as the reference
+  bf16* O = (bf16*)a.o + b * a.o_batch + qi * a.o_row + h * D;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    bf16x4 o4 = {(bf16)(ot[i][0] * inv), (bf16)(ot[i][1] * inv), (bf16)(ot[i][2] * inv), (bf16)(ot[i][3] * inv)};
+    *(bf16x4*)(O + i * 16 + g * 4) = o4;
+  }
+  if (a.lse && g == 0) a.lse[(b * H + h) * Lq + qi] = (m + __log2f(l)) * 0.6931471805599453f;
+}
+
 AttnK make_k(const mit_attn_args* x) {
   AttnK a;
   a.q = x->q; a.q_row = x->q_row; a.q_batch = x->q_batch;
@@ -295,7 +469,15 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
   AttnK a = make_k(x);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((Lq + 63) / 64), (unsigned)H, (unsigned)B);
-  if (dtype == MIT_BF16)
+  const bool mfma_ok = dtype == MIT_BF16 && x->q_row % 8 == 0 && x->q_batch % 8 == 0 && x->k_row % 8 == 0 &&
+                       x->k_batch % 8 == 0 && x->v_row % 8 == 0 && x->v_batch % 8 == 0 && x->o_row % 4 == 0 &&
+                       x->o_batch % 4 == 0 && ((uintptr_t)x->q | (uintptr_t)x->k | (uintptr_t)x->v) % 16 == 0 &&
+                       ((uintptr_t)x->o % 8) == 0 && getenv("MIT_ATTN_SIMPLE") == nullptr;
+  if (mfma_ok) {
+    const long kb = 2 * ((Lk - 1) * x->k_row + D), vb = 2 * ((Lk - 1) * x->v_row + D);
+    MIT_CHECK_ARG(kb < (1L << 31) && vb < (1L << 31), "mit_attention_fwd: K/V span >= 2 GiB");
+    hipLaunchKernelGGL(attn_fwd_mfma, grid, dim3(256), 0, s, H, Lq, Lk, a, (int)kb, (int)vb);
+  } else if (dtype == MIT_BF16)
     hipLaunchKernelGGL(attn_fwd_simple<bf16>, grid, dim3(64), 0, s, H, Lq, Lk, a);
   else
     hipLaunchKernelGGL(attn_fwd_simple<float>, grid, dim3(64), 0, s, H, Lq, Lk, a);

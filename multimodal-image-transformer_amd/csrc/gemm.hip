@@ -8,11 +8,18 @@
 //      MIT_MN_CONTIG -> B[k*ldb + n]      (W in dX = dY W, X in dW = dY^T X)
 //
 // bf16 path: 128x128x64 block tile, 4 waves (2x2), each wave 64x64 = 4x4 tiles of
-// v_mfma_f32_16x16x32_bf16, fp32 accumulation. Global -> registers -> LDS double buffer (one
-// barrier per K step). K-contig tiles are XOR-swizzled for conflict-free ds_read_b128 fragment
-// reads; MN-contig tiles are read with ds_read_b64_tr_b16 (CDNA4 hardware transpose) so the same
-// kernel serves NT / NN / TN without materialising a transpose.
-// fp32 path (parity mode): a plain LDS-tiled FMA kernel with the identical epilogue.
+// v_mfma_f32_16x16x32_bf16, fp32 accumulation.
+//   * staging: buffer loads (SRSRC descriptors) into registers -> LDS double buffer, one barrier
+//     per K step. Edge tiles need no branches: an out-of-range chunk gets an offset past the
+//     descriptor's num_records and the hardware returns zeros.
+//   * K-contig tiles are XOR-swizzled for conflict-free ds_read_b128 fragment reads; MN-contig
+//     tiles are read with ds_read_b64_tr_b16 (CDNA4 hardware transpose) so one kernel serves
+//     NT / NN / TN without materialising a transpose.
+//   * epilogue: the fp32 accumulator tile is staged through LDS, then every thread applies
+//     bias / activation / relu-dropout mask / dropout / residual to 8 consecutive columns and
+//     writes 16 bytes (coalesced rows instead of the MFMA layout's 4-row x 16-column scatter).
+//   * tile order: XCD-aware remap + 8-row grouping so tiles sharing A/B panels share an L2.
+// fp32 path (parity mode): a plain LDS-tiled FMA kernel with the identical epilogue semantics.
 #include "common.h"
 
 namespace {
@@ -33,15 +40,20 @@ struct Epi {
   uint32_t thresh;
   float dscale;
   int dropout;
+  int vec;  // 16-B vector epilogue legal (alignments / leading dims / N multiple of 8)
 };
 
-template <typename T>
-__device__ __forceinline__ void epi_store(const Epi& e, void* C, long ldc, long N, long r, long c, float v) {
-  v *= e.alpha;
-  if (e.bias) v += e.bias[c];
+__device__ __forceinline__ float epi_pre(const Epi& e, float v, float bias) {
+  v = v * e.alpha + bias;
   if (e.act == MIT_ACT_RELU) v = fmaxf(v, 0.0f);
   else if (e.act == MIT_ACT_GELU) v = gelu_erf(v);
   else if (e.act == MIT_ACT_QUICK_GELU) v = quick_gelu(v);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void epi_store(const Epi& e, void* C, long ldc, long N, long r, long c, float v) {
+  v = epi_pre(e, v, e.bias ? e.bias[c] : 0.0f);
   if (e.aux) v *= (to_f(((const T*)e.aux)[r * e.ld_aux + c]) > 0.0f) ? e.aux_scale : 0.0f;
   if (e.dropout) v *= drop_mul(site_key(e.seed, e.site), (uint64_t)r * (uint64_t)N + (uint64_t)c, e.thresh, e.dscale);
   if (e.res) v += to_f(((const T*)e.res)[r * e.ldr + c]);
@@ -54,39 +66,89 @@ __device__ __forceinline__ void epi_store(const Epi& e, void* C, long ldc, long 
   }
 }
 
+// 8 consecutive columns [c, c+8) of row r; vector loads / stores (bf16 operands)
+__device__ __forceinline__ void epi_store8_bf16(const Epi& e, void* C, long ldc, long N, long r, long c, float* v) {
+  float b[8];
+  if (e.bias) {
+    const f32x4 b0 = *(const f32x4*)(e.bias + c), b1 = *(const f32x4*)(e.bias + c + 4);
+    b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; b[3] = b0[3]; b[4] = b1[0]; b[5] = b1[1]; b[6] = b1[2]; b[7] = b1[3];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = epi_pre(e, v[k], b[k]);
+  if (e.aux) {
+    const bf16x8 a = *(const bf16x8*)((const bf16*)e.aux + r * e.ld_aux + c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= ((float)a[k] > 0.0f) ? e.aux_scale : 0.0f;
+  }
+  if (e.dropout) {
+    const uint64_t key = site_key(e.seed, e.site);
+    const uint64_t base = (uint64_t)r * (uint64_t)N + (uint64_t)c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= drop_mul(key, base + k, e.thresh, e.dscale);
+  }
+  if (e.res) {
+    const bf16x8 a = *(const bf16x8*)((const bf16*)e.res + r * e.ldr + c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += (float)a[k];
+  }
+  if (e.out_f32) {
+    f32x4* o = (f32x4*)((float*)C + r * ldc + c);
+    f32x4 lo = {v[0], v[1], v[2], v[3]}, hi = {v[4], v[5], v[6], v[7]};
+    if (e.accumulate) {
+      lo += o[0];
+      hi += o[1];
+    }
+    o[0] = lo;
+    o[1] = hi;
+  } else {
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+    *(bf16x8*)((bf16*)C + r * ldc + c) = o;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // bf16 MFMA kernel
 // ------------------------------------------------------------------------------------------------
 constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand per stage
+constexpr int TILE_BYTES = BM * BK * 2;          // 16 KiB per operand per stage
+constexpr int CST = BN + 4;                      // fp32 C-tile row stride in LDS (floats)
+constexpr int SMEM_BYTES = (4 * TILE_BYTES > BM * CST * 4) ? 4 * TILE_BYTES : BM * CST * 4;
+constexpr uint32_t OOB = 0x80000000u;            // buffer offset past any num_records -> loads 0
 
 // byte offset of 16-B chunk c (0..7) of row r in a K-contig [128][64] bf16 tile
 __device__ __forceinline__ int koff(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
-// swizzle of a k-row in an MN-contig [64][128] bf16 tile (256-B rows); see header comment
+// swizzle of a k-row in an MN-contig [64][128] bf16 tile (256-B rows): rows kr and kr+8 of a
+// 32-lane transposed read land in different 32-B bank groups
 __device__ __forceinline__ int mn_swz(int kr) { return ((kr & 3) | ((((kr >> 2) ^ (kr >> 3)) & 1) << 2)) << 5; }
 __device__ __forceinline__ int mnoff(int kr, int byte_in_row) { return kr * 256 + (byte_in_row ^ mn_swz(kr)); }
 
 template <int LAY>
 struct Stage {
   u32x4 r[4];
-  // load a BM(or BN) x BK tile starting at (row0 = m/n offset, k0) into registers
-  __device__ __forceinline__ void load(const bf16* __restrict__ g, long ld, long rows_total, long K, long row0, long k0, int tid) {
+  // BM (or BN) x BK tile at (row0 = m/n offset, k0) -> registers; out-of-range chunks read 0
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, long ld, long rows_total, long K, long row0, long k0,
+                                       int tid) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int id = tid + 256 * i;
       bool ok;
       long off;
       if (LAY == MIT_K_CONTIG) {
-        const int r = id >> 3, c = id & 7;
-        ok = (row0 + r < rows_total) && (k0 + c * 8 < K);
-        off = (row0 + r) * ld + k0 + c * 8;
+        const int rr = id >> 3, c = id & 7;
+        ok = (row0 + rr < rows_total) && (k0 + c * 8 < K);
+        off = (row0 + rr) * ld + k0 + c * 8;
       } else {
         const int kr = id >> 4, c = id & 15;
         ok = (k0 + kr < K) && (row0 + c * 8 < rows_total);
         off = (k0 + kr) * ld + row0 + c * 8;
       }
-      if (ok) r[i] = *(const u32x4*)(g + off);
-      else r[i] = u32x4{0u, 0u, 0u, 0u};
+      const uint32_t boff = ok ? (uint32_t)(off * 2) : OOB;
+      r[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)boff, 0, 0));
     }
   }
   __device__ __forceinline__ void store(char* lds, int tid) {
@@ -121,13 +183,14 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kk, int l
 
 template <int ALAY, int BLAY>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
-                                                        long M, long N, long K, long lda, long ldb, long ldc, Epi e) {
+                                                        long M, long N, long K, long lda, long ldb, long ldc,
+                                                        int a_bytes, int b_bytes, Epi e) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
-  // XCD-aware tile order: consecutive hardware block ids round-robin over 8 XCDs; give each
-  // XCD a contiguous run of tiles so neighbours share A/B panels in its L2 (guide §5.5 T1).
+  // XCD-aware tile order: hardware block ids round-robin over the 8 XCDs; give each XCD a
+  // contiguous run of tiles (bijective for any grid size) so neighbours share its L2 (guide §5.5 T1).
   const int nbn = (int)((N + BN - 1) / BN), nbm = (int)((M + BM - 1) / BM);
   const int nwg = nbn * nbm;
   int bid = blockIdx.x;
@@ -135,7 +198,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     const int q = nwg / 8, rr = nwg % 8, x = bid % 8, y = bid / 8;
     bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + y;
   }
-  // group tiles in column-panels of 8 M-blocks for L2 reuse of B
+  // groups of 8 M-blocks walk the N-blocks together (B panel reuse in L2)
   const int GROUP = 8;
   const int group_id = bid / (GROUP * nbn);
   const int first_m = group_id * GROUP;
@@ -144,7 +207,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   const int bn = (bid % (GROUP * nbn)) / gsize;
   const long m0 = (long)bm * BM, n0 = (long)bn * BN;
 
-  // stage buffer b: A tile at smem + b*2*TILE_BYTES, B tile right after it
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
+
 #define AS(b) (smem + (b) * 2 * TILE_BYTES)
 #define BS(b) (smem + (b) * 2 * TILE_BYTES + TILE_BYTES)
 
@@ -157,17 +222,18 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   Stage<ALAY> sa;
   Stage<BLAY> sb;
   const int nk = (int)((K + BK - 1) / BK);
-  sa.load(A, lda, M, K, m0, 0, tid);
-  sb.load(B, ldb, N, K, n0, 0, tid);
+  sa.load(ra, lda, M, K, m0, 0, tid);
+  sb.load(rb, ldb, N, K, n0, 0, tid);
   sa.store(AS(0), tid);
   sb.store(BS(0), tid);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      sa.load(A, lda, M, K, m0, (long)(kt + 1) * BK, tid);
-      sb.load(B, ldb, N, K, n0, (long)(kt + 1) * BK, tid);
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(ra, lda, M, K, m0, (long)(kt + 1) * BK, tid);
+      sb.load(rb, ldb, N, K, n0, (long)(kt + 1) * BK, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -181,27 +247,41 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) {
+    if (more) {
       sa.store(AS(cur ^ 1), tid);
       sb.store(BS(cur ^ 1), tid);
     }
     __syncthreads();
   }
+#undef AS
+#undef BS
 
+  // ---- epilogue: accumulators -> LDS (fp32 [128][CST]) -> 8-column vector rows ----
+  float* cs = (float*)smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long c = n0 + wn * 64 + j * 16 + (lane & 15);
-      if (c >= N) continue;
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const long r = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + t;
-        if (r < M) epi_store<bf16>(e, C, ldc, N, r, c, acc[i][j][t]);
-      }
+      for (int t = 0; t < 4; ++t)
+        cs[(wm * 64 + i * 16 + (lane >> 4) * 4 + t) * CST + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][t];
+  __syncthreads();
+#pragma unroll 2
+  for (int pass = 0; pass < (BM * BN / 8) / 256; ++pass) {
+    const int id = pass * 256 + tid;
+    const int r = id >> 4, c8 = (id & 15) * 8;
+    const long gr = m0 + r, gc = n0 + c8;
+    if (gr >= M || gc >= N) continue;
+    float v[8];
+    const f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3]; v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    if (e.vec && gc + 8 <= N) {
+      epi_store8_bf16(e, C, ldc, N, gr, gc, v);
+    } else {
+      for (int k = 0; k < 8; ++k)
+        if (gc + k < N) epi_store<bf16>(e, C, ldc, N, gr, gc + k, v[k]);
     }
-#undef AS
-#undef BS
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -258,10 +338,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 }
 
 template <int AL, int BL>
-void launch_bf16(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
+void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
   const long nbm = (g->M + BM - 1) / BM, nbn = (g->N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), dim3((unsigned)(nbm * nbn)), dim3(256), 4 * TILE_BYTES, s,
-                     (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, e);
+  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), dim3((unsigned)(nbm * nbn)), dim3(256), SMEM_BYTES, s,
+                     (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                     b_bytes, e);
 }
 template <int AL, int BL>
 void launch_f32(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
@@ -269,6 +350,8 @@ void launch_f32(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
   hipLaunchKernelGGL((gemm_f32_kernel<AL, BL>), grid, dim3(256), 0, s, (const float*)g->A, (const float*)g->B, g->C, g->M,
                      g->N, g->K, g->lda, g->ldb, g->ldc, e);
 }
+
+inline bool al16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 
 }  // namespace
 
@@ -286,6 +369,7 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   MIT_CHECK_ARG(g->ldb >= (g->b_layout == MIT_K_CONTIG ? g->K : g->N), "mit_gemm: ldb too small");
   MIT_CHECK_ARG(g->ldc >= g->N, "mit_gemm: ldc too small");
   MIT_CHECK_ARG(!g->accumulate || g->out_f32, "mit_gemm: accumulate needs an f32 output");
+  long a_bytes = 0, b_bytes = 0;
   if (g->dtype == MIT_BF16) {
     // 16-byte vector staging: contiguous extents and leading dims in multiples of 8 elements
     MIT_CHECK_ARG(g->lda % 8 == 0 && g->ldb % 8 == 0, "mit_gemm(bf16): lda/ldb must be multiples of 8");
@@ -293,7 +377,11 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
                   "mit_gemm(bf16): A's contiguous extent must be a multiple of 8");
     MIT_CHECK_ARG(g->b_layout == MIT_MN_CONTIG ? g->N % 8 == 0 : g->K % 8 == 0,
                   "mit_gemm(bf16): B's contiguous extent must be a multiple of 8");
-    MIT_CHECK_ARG(((uintptr_t)g->A % 16) == 0 && ((uintptr_t)g->B % 16) == 0, "mit_gemm(bf16): A/B must be 16-B aligned");
+    MIT_CHECK_ARG(al16(g->A) && al16(g->B), "mit_gemm(bf16): A/B must be 16-B aligned");
+    a_bytes = 2 * (g->a_layout == MIT_K_CONTIG ? (g->M - 1) * g->lda + g->K : (g->K - 1) * g->lda + g->M);
+    b_bytes = 2 * (g->b_layout == MIT_K_CONTIG ? (g->N - 1) * g->ldb + g->K : (g->K - 1) * g->ldb + g->N);
+    if (g->K == 0) a_bytes = b_bytes = 0;
+    MIT_CHECK_ARG(a_bytes < (1L << 31) && b_bytes < (1L << 31), "mit_gemm(bf16): operand spans >= 2 GiB");
   }
   Epi e;
   e.bias = g->bias;
@@ -311,19 +399,22 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   e.dropout = g->drop_p > 0.0f;
   e.thresh = drop_threshold(g->drop_p);
   e.dscale = g->drop_p < 1.0f ? 1.0f / (1.0f - g->drop_p) : 0.0f;
+  e.vec = (g->N % 8 == 0) && (g->ldc % 8 == 0) && al16(g->C) && (!g->bias || al16(g->bias)) &&
+          (!g->residual || (g->ldr % 8 == 0 && al16(g->residual))) && (!g->aux || (g->ld_aux % 8 == 0 && al16(g->aux)));
   hipStream_t s = (hipStream_t)stream;
   if (g->dtype == MIT_BF16) {
     if (!mit_gemm_smem_set) {
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TILE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
       mit_gemm_smem_set = true;
     }
-    if (g->a_layout == 0 && g->b_layout == 0) launch_bf16<0, 0>(g, e, s);
-    else if (g->a_layout == 0 && g->b_layout == 1) launch_bf16<0, 1>(g, e, s);
-    else if (g->a_layout == 1 && g->b_layout == 0) launch_bf16<1, 0>(g, e, s);
-    else launch_bf16<1, 1>(g, e, s);
+    const int ab = (int)a_bytes, bb = (int)b_bytes;
+    if (g->a_layout == 0 && g->b_layout == 0) launch_bf16<0, 0>(g, e, ab, bb, s);
+    else if (g->a_layout == 0 && g->b_layout == 1) launch_bf16<0, 1>(g, e, ab, bb, s);
+    else if (g->a_layout == 1 && g->b_layout == 0) launch_bf16<1, 0>(g, e, ab, bb, s);
+    else launch_bf16<1, 1>(g, e, ab, bb, s);
   } else {
     if (g->a_layout == 0 && g->b_layout == 0) launch_f32<0, 0>(g, e, s);
     else if (g->a_layout == 0 && g->b_layout == 1) launch_f32<0, 1>(g, e, s);

@@ -157,7 +157,22 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
     g = GemmArgs(dt, a_layout, b_layout, M, N, K, ptr(A), lda, ptr(B), ldb, ptr(C), ldc, alpha, ptr(bias), act,
                  ptr(residual), ldr if ldr is not None else ldc, ptr(aux), ld_aux if ld_aux is not None else ldc,
                  aux_scale, drop_p, ptr(seed), site, out_f32, 1 if accumulate else 0)
+    probe = _gemm_probe
+    if probe is not None:
+        probe.before(dt, a_layout, b_layout, M, N, K)
     _check(lib().mit_gemm(ctypes.byref(g), stream_ptr()), "mit_gemm")
+    if probe is not None:
+        probe.after()
+
+
+_gemm_probe = None
+
+
+def set_gemm_probe(probe):
+    """Install an object with before(dtype, a_layout, b_layout, M, N, K) / after() called around
+    every GEMM launch (bench.py records HIP events there to time the GEMM kernels in place)."""
+    global _gemm_probe
+    _gemm_probe = probe
 
 
 def linear(x, w, out, *, bias=None, act=ACT_NONE, residual=None, drop_p=0.0, seed=None, site=0):
