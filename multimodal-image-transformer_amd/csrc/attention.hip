@@ -443,6 +443,238 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
   if (a.lse && g == 0) a.lse[(b * H + h) * Lq + qi] = (m + __log2f(l)) * 0.6931471805599453f;
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16 MFMA backward, two kernels (launched dQ first: it also produces delta = rowsum(dO o O)).
+//   dQ kernel  (grid: query blocks): per 64-key tile  S^T = K Q^T, dP^T = V dO^T (A = K/V rows from
+//     LDS, B = Q/dO fragments in registers) -> dS^T -> dQ^T += K^T dS^T (A = K^T by transposed
+//     LDS read, B = dS^T from the accumulators, same permuted k index as the forward).
+//   dKV kernel (grid: key blocks, wave = 16 keys): per 64-query tile  S = Q K^T, dP = dO V^T
+//     (A = Q/dO rows from LDS, B = K/V fragments in registers; key on the lane) -> P, dS ->
+//     dV^T += dO^T (P o M), dK^T += Q^T dS (A by transposed LDS reads of the dO / Q tiles).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bf16x8 lds_row_frag(const char* tile, int row, int chunk) {
+  return __builtin_bit_cast(bf16x8, *(const u32x4*)(tile + koff_k(row, chunk)));
+}
+// A operand (m = column block [c0, c0+16) of the tile, k = rows kbase+{4g..4g+3, 16+4g..16+4g+3})
+__device__ __forceinline__ bf16x8 lds_tr_frag(const char* tile, int kbase, int c0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int colb = (c0 + 4 * p) * 2;
+  const int r0 = kbase + g * 4 + q;
+  // koff_k chunk swizzle applied to the 8-byte half-chunk the lane reads
+  auto addr = [&](int r) { return r * 128 + ((((colb >> 4) ^ ((r >> 1) & 7)) << 4) | (colb & 15)); };
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, tile + addr(r0)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, tile + addr(r0 + 16)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ void load_tile_rows(char* tile, const bf16* base, long row_stride, long r0, long nrows, int bytes,
+                                               int tid) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + 256 * i, r = id >> 3, c = id & 7;
+    const long row = r0 + r;
+    const uint32_t off = row < nrows ? (uint32_t)((row * row_stride + c * 8) * 2) : A_OOB;
+    *(u32x4*)(tile + koff_k(r, c)) = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+  }
+}
+
+struct AttnBwdBytes {
+  int q, k, v, dO;
+};
+
+__global__ __launch_bounds__(256) void attn_bwd_dq_mfma(long H, long Lq, long Lk, AttnK a, AttnG gr, AttnBwdBytes nb_) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * AK * D * 2];  // K tile, V tile
+  char* Ks = lds;
+  char* Vs = lds + AK * D * 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const long b = blockIdx.z, h = blockIdx.y;
+  const long qblk = (long)blockIdx.x * AQ;
+  const long qi = qblk + w * 16 + (lane & 15);
+  const bool qlive = qi < Lq;
+  const long qr = qlive ? qi : 0;
+  const bf16* Qr = (const bf16*)a.q + b * a.q_batch + h * D + qr * a.q_row;
+  const bf16* Or = (const bf16*)a.o + b * a.o_batch + h * D + qr * a.o_row;
+  const bf16* dOr = (const bf16*)gr.dout + b * gr.do_batch + h * D + qr * gr.do_row;
+  bf16x8 qf[2], df[2];
+  float delta = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    u32x4 qv = *(const u32x4*)(Qr + kk * 32 + g * 8), dv = *(const u32x4*)(dOr + kk * 32 + g * 8);
+    const bf16x8 ov = __builtin_bit_cast(bf16x8, *(const u32x4*)(Or + kk * 32 + g * 8));
+    if (!qlive) qv = dv = u32x4{0u, 0u, 0u, 0u};
+    qf[kk] = __builtin_bit_cast(bf16x8, qv);
+    df[kk] = __builtin_bit_cast(bf16x8, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) delta += (float)df[kk][j] * (float)ov[j];
+  }
+  delta += __shfl_xor(delta, 16, 64);
+  delta += __shfl_xor(delta, 32, 64);
+  const long row = (b * H + h) * Lq + qi;
+  if (qlive && g == 0) gr.delta[row] = delta;
+  const float l2e = 1.4426950408889634f;
+  const float lse2 = qlive ? a.lse[row] * l2e : 0.f;
+  const float sl2 = a.scale * l2e;
+  const uint64_t key = a.dropout ? site_key(a.seed, a.site) : 0ull;
+  const uint64_t rowbase = (uint64_t)row * (uint64_t)Lk;
+  const int64_t* tok = a.tok ? a.tok + b * a.tok_batch : nullptr;
+  const bf16* Kb = (const bf16*)a.k + b * a.k_batch + h * D;
+  const bf16* Vb = (const bf16*)a.v + b * a.v_batch + h * D;
+  long kend = Lk;
+  if (a.causal) kend = min(Lk, min(Lq, qblk + AQ));
+  f32x4 dq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (long j0 = 0; j0 < kend; j0 += AK) {
+    __syncthreads();
+    load_tile_rows(Ks, Kb, a.k_row, j0, Lk, nb_.k, tid);
+    load_tile_rows(Vs, Vb, a.v_row, j0, Lk, nb_.v, tid);
+    __syncthreads();
+    f32x4 st[4], dp[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) st[nb] = dp[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_row_frag(Ks, nb * 16 + (lane & 15), kk * 4 + g), qf[kk],
+                                                         st[nb], 0, 0, 0);
+        dp[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_row_frag(Vs, nb * 16 + (lane & 15), kk * 4 + g), df[kk],
+                                                         dp[nb], 0, 0, 0);
+      }
+    float ds[16];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const long kj = j0 + nb * 16 + g * 4 + t;
+        bool msk = !qlive || kj >= Lk || (a.causal && kj > qi);
+        if (!msk && tok) msk = tok[kj] == a.pad;
+        const float p = msk ? 0.f : exp2f(st[nb][t] * sl2 - lse2);
+        const float mul = a.dropout ? drop_mul(key, rowbase + (uint64_t)kj, a.thresh, a.dscale) : 1.f;
+        ds[nb * 4 + t] = p * (dp[nb][t] * mul - delta);
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bs;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bs[j] = (bf16)ds[(2 * kk) * 4 + j];
+        bs[4 + j] = (bf16)ds[(2 * kk + 1) * 4 + j];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dq[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_tr_frag(Ks, kk * 32, i * 16, lane), bs,
+                                                                              dq[i], 0, 0, 0);
+    }
+  }
+  if (!qlive) return;
+  bf16* DQ = (bf16*)gr.dq + b * gr.dq_batch + qi * gr.dq_row + h * D;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    *(bf16x4*)(DQ + i * 16 + g * 4) = bf16x4{(bf16)(dq[i][0] * a.scale), (bf16)(dq[i][1] * a.scale),
+                                             (bf16)(dq[i][2] * a.scale), (bf16)(dq[i][3] * a.scale)};
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkv_mfma(long H, long Lq, long Lk, AttnK a, AttnG gr, AttnBwdBytes nb_) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * AQ * D * 2 + 2 * AQ * 4];  // Q tile, dO tile, lse, delta
+  char* Qs = lds;
+  char* Ds = lds + AQ * D * 2;
+  float* Ls = (float*)(lds + 2 * AQ * D * 2);
+  float* Dl = Ls + AQ;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const long b = blockIdx.z, h = blockIdx.y;
+  const long kblk = (long)blockIdx.x * AK;
+  const long kl = kblk + w * 16 + (lane & 15);
+  const bool klive = kl < Lk;
+  const long kr = klive ? kl : 0;
+  const bf16* Kr = (const bf16*)a.k + b * a.k_batch + h * D + kr * a.k_row;
+  const bf16* Vr = (const bf16*)a.v + b * a.v_batch + h * D + kr * a.v_row;
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    u32x4 k4 = *(const u32x4*)(Kr + kk * 32 + g * 8), v4 = *(const u32x4*)(Vr + kk * 32 + g * 8);
+    if (!klive) k4 = v4 = u32x4{0u, 0u, 0u, 0u};
+    kf[kk] = __builtin_bit_cast(bf16x8, k4);
+    vf[kk] = __builtin_bit_cast(bf16x8, v4);
+  }
+  const bool kpad = klive && a.tok && a.tok[b * a.tok_batch + kl] == a.pad;
+  const float l2e = 1.4426950408889634f;
+  const float sl2 = a.scale * l2e;
+  const uint64_t key = a.dropout ? site_key(a.seed, a.site) : 0ull;
+  const bf16* Qb = (const bf16*)a.q + b * a.q_batch + h * D;
+  const bf16* dOb = (const bf16*)gr.dout + b * gr.do_batch + h * D;
+  const long bh = b * H + h;
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const long qstart = a.causal ? (kblk / AQ) * AQ : 0;  // queries before the block's first key see none of it
+  for (long q0 = qstart; q0 < Lq; q0 += AQ) {
+    __syncthreads();
+    load_tile_rows(Qs, Qb, a.q_row, q0, Lq, nb_.q, tid);
+    load_tile_rows(Ds, dOb, gr.do_row, q0, Lq, nb_.dO, tid);
+    if (tid < AQ) {
+      const long q = q0 + tid;
+      Ls[tid] = q < Lq ? a.lse[bh * Lq + q] * l2e : 0.f;
+      Dl[tid] = q < Lq ? gr.delta[bh * Lq + q] : 0.f;
+    }
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) s[nb] = dp[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        s[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_row_frag(Qs, nb * 16 + (lane & 15), kk * 4 + g), kf[kk], s[nb],
+                                                        0, 0, 0);
+        dp[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_row_frag(Ds, nb * 16 + (lane & 15), kk * 4 + g), vf[kk],
+                                                         dp[nb], 0, 0, 0);
+      }
+    float pd[16], ds[16];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int qq = nb * 16 + g * 4 + t;
+        const long q = q0 + qq;
+        const bool msk = !klive || kpad || q >= Lq || (a.causal && kl > q);
+        const float p = msk ? 0.f : exp2f(s[nb][t] * sl2 - Ls[qq]);
+        const float mul = a.dropout ? drop_mul(key, ((uint64_t)bh * (uint64_t)Lq + (uint64_t)q) * (uint64_t)Lk + kl, a.thresh,
+                                               a.dscale)
+                                    : 1.f;
+        pd[nb * 4 + t] = p * mul;
+        ds[nb * 4 + t] = p * (dp[nb][t] * mul - Dl[qq]);
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bp, bs;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bp[j] = (bf16)pd[(2 * kk) * 4 + j];
+        bp[4 + j] = (bf16)pd[(2 * kk + 1) * 4 + j];
+        bs[j] = (bf16)ds[(2 * kk) * 4 + j];
+        bs[4 + j] = (bf16)ds[(2 * kk + 1) * 4 + j];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dv[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_tr_frag(Ds, kk * 32, i * 16, lane), bp, dv[i], 0, 0, 0);
+        dk[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_tr_frag(Qs, kk * 32, i * 16, lane), bs, dk[i], 0, 0, 0);
+      }
+    }
+  }
+  if (!klive) return;
+  bf16* DK = (bf16*)gr.dk + b * gr.dk_batch + kl * gr.dk_row + h * D;
+  bf16* DV = (bf16*)gr.dv + b * gr.dv_batch + kl * gr.dv_row + h * D;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    *(bf16x4*)(DK + i * 16 + g * 4) = bf16x4{(bf16)(dk[i][0] * a.scale), (bf16)(dk[i][1] * a.scale),
+                                             (bf16)(dk[i][2] * a.scale), (bf16)(dk[i][3] * a.scale)};
+    *(bf16x4*)(DV + i * 16 + g * 4) = bf16x4{(bf16)dv[i][0], (bf16)dv[i][1], (bf16)dv[i][2], (bf16)dv[i][3]};
+  }
+}
+
 AttnK make_k(const mit_attn_args* x) {
   AttnK a;
   a.q = x->q; a.q_row = x->q_row; a.q_batch = x->q_batch;
@@ -501,7 +733,27 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
   hipStream_t s = (hipStream_t)stream;
   dim3 gq((unsigned)((Lq + 63) / 64), (unsigned)H, (unsigned)B);
   dim3 gk((unsigned)((Lk + 63) / 64), (unsigned)H, (unsigned)B);
-  if (dtype == MIT_BF16) {
+  auto al = [](const void* p, int n) { return ((uintptr_t)p % n) == 0; };
+  const bool mfma_ok = dtype == MIT_BF16 && x->q_row % 8 == 0 && x->q_batch % 8 == 0 && x->k_row % 8 == 0 &&
+                       x->k_batch % 8 == 0 && x->v_row % 8 == 0 && x->v_batch % 8 == 0 && x->o_row % 8 == 0 &&
+                       x->o_batch % 8 == 0 && gg->do_row % 8 == 0 && gg->do_batch % 8 == 0 && gg->dq_row % 4 == 0 &&
+                       gg->dq_batch % 4 == 0 && gg->dk_row % 4 == 0 && gg->dk_batch % 4 == 0 && gg->dv_row % 4 == 0 &&
+                       gg->dv_batch % 4 == 0 && al(x->q, 16) && al(x->k, 16) && al(x->v, 16) && al(x->o, 16) &&
+                       al(gg->dout, 16) && al(gg->dq, 8) && al(gg->dk, 8) && al(gg->dv, 8) &&
+                       getenv("MIT_ATTN_SIMPLE") == nullptr;
+  if (mfma_ok) {
+    AttnBwdBytes nb;
+    const long qb = 2 * ((Lq - 1) * x->q_row + D), kb = 2 * ((Lk - 1) * x->k_row + D);
+    const long vb = 2 * ((Lk - 1) * x->v_row + D), db = 2 * ((Lq - 1) * gg->do_row + D);
+    MIT_CHECK_ARG(qb < (1L << 31) && kb < (1L << 31) && vb < (1L << 31) && db < (1L << 31),
+                  "mit_attention_bwd: operand span >= 2 GiB");
+    nb.q = (int)qb;
+    nb.k = (int)kb;
+    nb.v = (int)vb;
+    nb.dO = (int)db;
+    hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 0, s, H, Lq, Lk, a, g, nb);
+    hipLaunchKernelGGL(attn_bwd_dkv_mfma, gk, dim3(256), 0, s, H, Lq, Lk, a, g, nb);
+  } else if (dtype == MIT_BF16) {
     hipLaunchKernelGGL(attn_bwd_dq_simple<bf16>, gq, dim3(64), 0, s, H, Lq, Lk, a, g);
     hipLaunchKernelGGL(attn_bwd_dkv_simple<bf16>, gk, dim3(64), 0, s, H, Lq, Lk, a, g);
   } else {
