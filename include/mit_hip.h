@@ -51,6 +51,10 @@ int mit_abi_version(void);
  *   auxmask: if aux != NULL, multiply by (aux[m*ld_aux+n] > 0 ? aux_scale : 0)  (ReLU/dropout bwd)
  *   dropout index = m*N + n ; residual/aux in the operand dtype; bias f32 [N]
  *   out_f32: write f32 (accumulate: C += value), else the operand dtype.
+ *   rowsum (optional, f32 [M]): rowsum[m] = sum_k A(m,k) — the bias gradient when A = dY^T in a
+ *     weight-gradient GEMM, fused in (no separate column-sum pass over dY).
+ *   workspace: scratch for split-K (plain-epilogue GEMMs with few output tiles and a long K, i.e.
+ *     weight gradients); size from mit_gemm_workspace_bytes(M, N, K). NULL / too small -> no split.
  * bf16 requirements: lda, ldb and the contiguous extent of each operand multiples of 8; A, B 16-B aligned. */
 typedef struct {
   int dtype, a_layout, b_layout;
@@ -74,8 +78,12 @@ typedef struct {
   uint32_t site;
   int out_f32;
   int accumulate;
+  float* rowsum;
+  void* workspace;
+  long workspace_bytes;
 } mit_gemm_args;
 int mit_gemm(const mit_gemm_args* args, void* stream);
+long mit_gemm_workspace_bytes(long M, long N, long K);
 
 /* ---------------------------------------------------------------------------------------------
  * LayerNorm over the last dim, fp32 statistics.

@@ -184,7 +184,8 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kk, int l
 template <int ALAY, int BLAY>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                         long M, long N, long K, long lda, long ldb, long ldc,
-                                                        int a_bytes, int b_bytes, Epi e) {
+                                                        int a_bytes, int b_bytes, Epi e, int ksplit, long kchunk,
+                                                        float* __restrict__ ws, float* __restrict__ rowsum) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -192,12 +193,16 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   // XCD-aware tile order: hardware block ids round-robin over the 8 XCDs; give each XCD a
   // contiguous run of tiles (bijective for any grid size) so neighbours share its L2 (guide §5.5 T1).
   const int nbn = (int)((N + BN - 1) / BN), nbm = (int)((M + BM - 1) / BM);
-  const int nwg = nbn * nbm;
+  const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
   int bid = blockIdx.x;
   {
     const int q = nwg / 8, rr = nwg % 8, x = bid % 8, y = bid / 8;
     bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + y;
   }
+  // split-K: slice `split` covers k in [kb, ke)
+  const int split = bid / ntiles;
+  bid -= split * ntiles;
+  const long kb = (long)split * kchunk, ke = min(K, kb + kchunk);
   // groups of 8 M-blocks walk the N-blocks together (B panel reuse in L2)
   const int GROUP = 8;
   const int group_id = bid / (GROUP * nbn);
@@ -219,11 +224,21 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // fused row sums of A (bias gradients): one extra MFMA against a ones fragment, only in the
+  // blocks of the first column tile and the waves of its first column half (wave-uniform branch)
+  // (compiled only into the TN instance — the weight-gradient GEMMs — so the other instances
+  // keep their register budget)
+  const bool do_rs = ALAY == MIT_MN_CONTIG && BLAY == MIT_MN_CONTIG && rowsum != nullptr && bn == 0 && wn == 0;
+  // per lane: partial row sums of its 8 k-values of rows rbase + (lane&15), via v_dot2_f32_bf16
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  const bf16x2 one2 = {(bf16)1.0f, (bf16)1.0f};
+
   Stage<ALAY> sa;
   Stage<BLAY> sb;
-  const int nk = (int)((K + BK - 1) / BK);
-  sa.load(ra, lda, M, K, m0, 0, tid);
-  sb.load(rb, ldb, N, K, n0, 0, tid);
+  const int nk = (int)((ke - kb + BK - 1) / BK);
+  sa.load(ra, lda, M, ke, m0, kb, tid);
+  sb.load(rb, ldb, N, ke, n0, kb, tid);
   sa.store(AS(0), tid);
   sb.store(BS(0), tid);
   __syncthreads();
@@ -232,8 +247,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      sa.load(ra, lda, M, K, m0, (long)(kt + 1) * BK, tid);
-      sb.load(rb, ldb, N, K, n0, (long)(kt + 1) * BK, tid);
+      sa.load(ra, lda, M, ke, m0, kb + (long)(kt + 1) * BK, tid);
+      sb.load(rb, ldb, N, ke, n0, kb + (long)(kt + 1) * BK, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -246,6 +261,15 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (do_rs) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          rs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(af[i], af[i], 0, 1), one2, rs[i], false);
+          rs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(af[i], af[i], 2, 3), one2, rs[i], false);
+          rs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(af[i], af[i], 4, 5), one2, rs[i], false);
+          rs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(af[i], af[i], 6, 7), one2, rs[i], false);
+        }
+      }
     }
     if (more) {
       sa.store(AS(cur ^ 1), tid);
@@ -265,6 +289,18 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         cs[(wm * 64 + i * 16 + (lane >> 4) * 4 + t) * CST + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][t];
+  if (do_rs) {
+    // lanes l, l+16, l+32, l+48 hold the four k-groups of row (l & 15): reduce across them
+    float* dst = ksplit > 1 ? ws + (long)ksplit * M * N + (long)split * M : rowsum;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const long r = m0 + wm * 64 + i * 16 + (lane & 15);
+      if (lane < 16 && r < M) dst[r] = v;
+    }
+  }
   __syncthreads();
 #pragma unroll 2
   for (int pass = 0; pass < (BM * BN / 8) / 256; ++pass) {
@@ -274,6 +310,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     if (gr >= M || gc >= N) continue;
     float v[8];
     const f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
+    if (ksplit > 1) {  // raw fp32 partial slab; gemm_splitk_reduce applies the (plain) epilogue
+      f32x4* o = (f32x4*)(ws + ((long)split * M + gr) * N + gc);
+      o[0] = lo;
+      o[1] = hi;
+      continue;
+    }
     v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3]; v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
     if (e.vec && gc + 8 <= N) {
       epi_store8_bf16(e, C, ldc, N, gr, gc, v);
@@ -284,18 +326,66 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   }
 }
 
+// C = alpha * sum_s slab[s] (f32 or bf16 out, optional accumulate); rowsum = sum_s rowslab[s]
+__global__ void gemm_splitk_reduce(long M, long N, int ksplit, const float* __restrict__ ws, void* C, long ldc,
+                                   float alpha, int out_f32, int accumulate, float* rowsum) {
+  const long n4 = N / 4, total = M * n4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / n4, c = (i % n4) * 4;
+    f32x4 s = *(const f32x4*)(ws + r * N + c);
+    for (int k = 1; k < ksplit; ++k) s += *(const f32x4*)(ws + ((long)k * M + r) * N + c);
+    s *= alpha;
+    if (out_f32) {
+      f32x4* o = (f32x4*)((float*)C + r * ldc + c);
+      if (accumulate) s += *o;
+      *o = s;
+    } else {
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      *(bf16x4*)((bf16*)C + r * ldc + c) = bf16x4{(bf16)s[0], (bf16)s[1], (bf16)s[2], (bf16)s[3]};
+    }
+  }
+  if (rowsum) {
+    const float* rw = ws + (long)ksplit * M * N;
+    for (long r = (long)blockIdx.x * blockDim.x + threadIdx.x; r < M; r += (long)gridDim.x * blockDim.x) {
+      float s = 0.f;
+      for (int k = 0; k < ksplit; ++k) s += rw[(long)k * M + r];
+      rowsum[r] = s;
+    }
+  }
+}
+
+// split-K plan for a plain-epilogue bf16 GEMM: only when the output has too few 128x128 tiles to
+// fill 256 CUs and K is long (the weight-gradient shapes). Returns 1 (no split) otherwise.
+int splitk_plan(long M, long N, long K, long* kchunk) {
+  const long tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  *kchunk = K;
+  if (tiles >= 256 || K < 1024 || N % 8) return 1;
+  long s = (512 + tiles - 1) / tiles;
+  s = min(s, K / 512);
+  s = min(s, 16L);
+  if (s < 2) return 1;
+  long kc = (K + s - 1) / s;
+  kc = (kc + BK - 1) / BK * BK;
+  *kchunk = kc;
+  return (int)((K + kc - 1) / kc);
+}
+long splitk_ws_bytes(long M, long N, int s) { return s > 1 ? 4L * s * M * N + 4L * s * M : 0; }
+
 // ------------------------------------------------------------------------------------------------
 // fp32 FMA kernel (parity mode): 64x64x16 tile, 256 threads x (4x4) outputs
 // ------------------------------------------------------------------------------------------------
 template <int ALAY, int BLAY>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, const float* __restrict__ B, void* C,
-                                                       long M, long N, long K, long lda, long ldb, long ldc, Epi e) {
+                                                       long M, long N, long K, long lda, long ldb, long ldc, Epi e,
+                                                       float* __restrict__ rowsum) {
   __shared__ float As[16][64 + 4];
   __shared__ float Bs[16][64 + 4];
   const int tid = threadIdx.x;
   const long m0 = (long)blockIdx.y * 64, n0 = (long)blockIdx.x * 64;
   const int tm = (tid >> 4) * 4, tn = (tid & 15) * 4;
   float acc[4][4] = {};
+  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool do_rs = rowsum != nullptr && blockIdx.x == 0 && tn == 0;
   for (long k0 = 0; k0 < K; k0 += 16) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -325,6 +415,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+      if (do_rs) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rsum[i] += a[i];
+      }
     }
     __syncthreads();
   }
@@ -335,20 +429,26 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
       const long r = m0 + tm + i, c = n0 + tn + j;
       if (r < M && c < N) epi_store<float>(e, C, ldc, N, r, c, acc[i][j]);
     }
+  if (do_rs) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (m0 + tm + i < M) rowsum[m0 + tm + i] = rsum[i];
+  }
 }
 
 template <int AL, int BL>
-void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, int ksplit, long kchunk,
+                 hipStream_t s) {
   const long nbm = (g->M + BM - 1) / BM, nbn = (g->N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), dim3((unsigned)(nbm * nbn)), dim3(256), SMEM_BYTES, s,
+  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), dim3((unsigned)(nbm * nbn * ksplit)), dim3(256), SMEM_BYTES, s,
                      (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                     b_bytes, e);
+                     b_bytes, e, ksplit, kchunk, (float*)g->workspace, g->rowsum);
 }
 template <int AL, int BL>
 void launch_f32(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
   dim3 grid((unsigned)((g->N + 63) / 64), (unsigned)((g->M + 63) / 64));
   hipLaunchKernelGGL((gemm_f32_kernel<AL, BL>), grid, dim3(256), 0, s, (const float*)g->A, (const float*)g->B, g->C, g->M,
-                     g->N, g->K, g->lda, g->ldb, g->ldc, e);
+                     g->N, g->K, g->lda, g->ldb, g->ldc, e, g->rowsum);
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p % 16) == 0; }
@@ -356,6 +456,11 @@ inline bool al16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 }  // namespace
 
 static bool mit_gemm_smem_set = false;
+
+extern "C" long mit_gemm_workspace_bytes(long M, long N, long K) {
+  long kc;
+  return splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc));
+}
 
 extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   MIT_CHECK_ARG(g != nullptr, "mit_gemm: null args");
@@ -369,6 +474,8 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   MIT_CHECK_ARG(g->ldb >= (g->b_layout == MIT_K_CONTIG ? g->K : g->N), "mit_gemm: ldb too small");
   MIT_CHECK_ARG(g->ldc >= g->N, "mit_gemm: ldc too small");
   MIT_CHECK_ARG(!g->accumulate || g->out_f32, "mit_gemm: accumulate needs an f32 output");
+  MIT_CHECK_ARG(!g->rowsum || g->dtype == MIT_F32 || (g->a_layout == MIT_MN_CONTIG && g->b_layout == MIT_MN_CONTIG),
+                "mit_gemm(bf16): rowsum is fused into the weight-gradient (MN, MN) layout only");
   long a_bytes = 0, b_bytes = 0;
   if (g->dtype == MIT_BF16) {
     // 16-byte vector staging: contiguous extents and leading dims in multiples of 8 elements
@@ -411,10 +518,29 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
       mit_gemm_smem_set = true;
     }
     const int ab = (int)a_bytes, bb = (int)b_bytes;
-    if (g->a_layout == 0 && g->b_layout == 0) launch_bf16<0, 0>(g, e, ab, bb, s);
-    else if (g->a_layout == 0 && g->b_layout == 1) launch_bf16<0, 1>(g, e, ab, bb, s);
-    else if (g->a_layout == 1 && g->b_layout == 0) launch_bf16<1, 0>(g, e, ab, bb, s);
-    else launch_bf16<1, 1>(g, e, ab, bb, s);
+    long kchunk = g->K;
+    int ks = 1;
+    const bool plain = !g->bias && g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f;
+    if (plain && g->workspace) {
+      ks = splitk_plan(g->M, g->N, g->K, &kchunk);
+      if (ks > 1 && (splitk_ws_bytes(g->M, g->N, ks) > g->workspace_bytes || !al16(g->workspace) ||
+                     (g->out_f32 ? false : (g->ldc % 4 != 0)) || g->ldc % 4 != 0 || !al16(g->C))) {
+        ks = 1;
+        kchunk = g->K;
+      }
+    }
+    if (g->a_layout == 0 && g->b_layout == 0) launch_bf16<0, 0>(g, e, ab, bb, ks, kchunk, s);
+    else if (g->a_layout == 0 && g->b_layout == 1) launch_bf16<0, 1>(g, e, ab, bb, ks, kchunk, s);
+    else if (g->a_layout == 1 && g->b_layout == 0) launch_bf16<1, 0>(g, e, ab, bb, ks, kchunk, s);
+    else launch_bf16<1, 1>(g, e, ab, bb, ks, kchunk, s);
+    if (ks > 1) {
+      MIT_LAUNCH_CHECK("mit_gemm");
+      const long total = g->M * (g->N / 4);
+      long blocks = (total + 255) / 256;
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, g->M, g->N, ks,
+                         (const float*)g->workspace, g->C, g->ldc, g->alpha, g->out_f32, g->accumulate, g->rowsum);
+    }
   } else {
     if (g->a_layout == 0 && g->b_layout == 0) launch_f32<0, 0>(g, e, s);
     else if (g->a_layout == 0 && g->b_layout == 1) launch_f32<0, 1>(g, e, s);

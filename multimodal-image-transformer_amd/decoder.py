@@ -127,7 +127,7 @@ def flat_to_reference(store: FlatParams, L: int, d: int, prefix: str = "decoder.
 class _Acts:
     """Activation arena for one (B, T, S, train) shape; allocated once, reused every step."""
 
-    def __init__(self, B, T, S, d, F, L, V, H, dt, dev, train: bool):
+    def __init__(self, B, T, S, d, F, L, V, H, dt, dev, train: bool, proj_in: Optional[int] = None):
         R = B * T
         e = lambda *s: torch.empty(*s, dtype=dt, device=dev)  # noqa: E731
         f = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
@@ -162,8 +162,12 @@ class _Acts:
             self.dmem = e(B * S, d)
             self.delta = f(B * H * T)
             self.ln_ws = f(native.layernorm_bwd_ws_floats(R, d))
-            self.cs_ws = f(max(native.colsum_ws_floats(R, max(V, F, 3 * d)),
-                               native.colsum_ws_floats(B * S, L * 2 * d)))
+            # split-K scratch for the weight-gradient GEMMs (and the long-K dX GEMMs)
+            E = proj_in or d
+            shapes = [(V, d, R), (d, F, R), (F, d, R), (d, d, R), (3 * d, d, R), (L * 2 * d, d, B * S), (d, E, B * S),
+                      (R, d, V), (B * S, d, L * 2 * d)]
+            need = max(native.gemm_workspace_bytes(m, n, k) for m, n, k in shapes)
+            self.gemm_ws = torch.empty(max(need, 16) // 4 + 4, dtype=torch.float32, device=dev)
 
 
 class TransformerDecoder:
@@ -243,7 +247,9 @@ class TransformerDecoder:
     def acts(self, B, T, S, train) -> _Acts:
         key = (B, T, S, train)
         if key not in self._acts:
-            self._acts[key] = _Acts(B, T, S, self.d, self.F, self.L, self.V, self.H, self.dtype, self.device, train)
+            pi = self.store.index.get("projection.weight")
+            self._acts[key] = _Acts(B, T, S, self.d, self.F, self.L, self.V, self.H, self.dtype, self.device, train,
+                                    proj_in=pi[0][1] if pi else None)
         return self._acts[key]
 
     def _p(self):
@@ -315,10 +321,16 @@ class TransformerDecoder:
         R = B * T
         MN, K = native.MN_CONTIG, native.K_CONTIG
         x_last = A.xs[L - 1][2]
+        ws = A.gemm_ws
+
+        def dW(dy, x, wname, bname, M, N, K, lda, ldb):
+            """weight grad dY^T X (TN GEMM) with the bias grad (row sums of dY^T) fused in, split-K."""
+            native.gemm(dy, x, g(wname), M, N, K, a_layout=MN, b_layout=MN, lda=lda, ldb=ldb, rowsum=g(bname),
+                        workspace=ws)
+
         # fc_out
-        native.gemm(dlogits, x_last, g("fc_out.weight"), V, d, R, a_layout=MN, b_layout=MN, lda=V, ldb=d)
-        native.colsum(dlogits, R, V, g("fc_out.bias"), A.cs_ws)
-        native.gemm(dlogits, w("fc_out.weight"), A.dx, R, d, V, b_layout=MN, ldb=d)
+        dW(dlogits, x_last, "fc_out.weight", "fc_out.bias", V, d, R, V, d)
+        native.gemm(dlogits, w("fc_out.weight"), A.dx, R, d, V, b_layout=MN, ldb=d, workspace=ws)
         if grads_ready:
             grads_ready("fc_out.weight", "fc_out.bias")
         ascale = 1.0 / (1.0 - p) if p > 0 else 1.0
@@ -332,20 +344,17 @@ class TransformerDecoder:
                                  g(pre + "norm3.weight"), g(pre + "norm3.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
                                  site=base + 5)
             # FFN
-            native.gemm(A.dy, A.h[l], g(pre + "linear2.weight"), d, F, R, a_layout=MN, b_layout=MN, lda=d, ldb=F)
-            native.colsum(A.dy, R, d, g(pre + "linear2.bias"), A.cs_ws)
+            dW(A.dy, A.h[l], pre + "linear2.weight", pre + "linear2.bias", d, F, R, d, F)
             native.gemm(A.dy, w(pre + "linear2.weight"), A.dh, R, F, d, b_layout=MN, ldb=F, aux=A.h[l], ld_aux=F,
                         aux_scale=ascale)
-            native.gemm(A.dh, xs[1], g(pre + "linear1.weight"), F, d, R, a_layout=MN, b_layout=MN, lda=F, ldb=d)
-            native.colsum(A.dh, R, F, g(pre + "linear1.bias"), A.cs_ws)
+            dW(A.dh, xs[1], pre + "linear1.weight", pre + "linear1.bias", F, d, R, F, d)
             native.gemm(A.dh, w(pre + "linear1.weight"), A.dx, R, d, F, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
             # LN2
             native.layernorm_bwd(A.dx, z[1], stt[1][0], stt[1][1], st.p(pre + "norm2.weight"), A.dx,
                                  g(pre + "norm2.weight"), g(pre + "norm2.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
                                  site=base + 3)
             # cross-attention block
-            native.gemm(A.dy, A.oc[l], g(pre + "cross_out.weight"), d, d, R, a_layout=MN, b_layout=MN, lda=d, ldb=d)
-            native.colsum(A.dy, R, d, g(pre + "cross_out.bias"), A.cs_ws)
+            dW(A.dy, A.oc[l], pre + "cross_out.weight", pre + "cross_out.bias", d, d, R, d, d)
             native.gemm(A.dy, w(pre + "cross_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d)
             kvl, dkvl = A.kv[:, l * 2 * d:], A.dkv[:, l * 2 * d:]
             ca = native.attn_args(A.qc[l], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
@@ -354,16 +363,14 @@ class TransformerDecoder:
             cg = native.attn_grads(A.do, d, T * d, A.dq, d, T * d, dkvl, L * 2 * d, S * L * 2 * d, dkvl[:, d:],
                                    L * 2 * d, S * L * 2 * d, A.delta)
             native.attention_bwd(native.dtype_code(A.dq), B, H, T, S, ca, cg)
-            native.gemm(A.dq, xs[0], g(pre + "cross_q.weight"), d, d, R, a_layout=MN, b_layout=MN, lda=d, ldb=d)
-            native.colsum(A.dq, R, d, g(pre + "cross_q.bias"), A.cs_ws)
+            dW(A.dq, xs[0], pre + "cross_q.weight", pre + "cross_q.bias", d, d, R, d, d)
             native.gemm(A.dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
             # LN1
             native.layernorm_bwd(A.dx, z[0], stt[0][0], stt[0][1], st.p(pre + "norm1.weight"), A.dx,
                                  g(pre + "norm1.weight"), g(pre + "norm1.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
                                  site=base + 1)
             # self-attention block
-            native.gemm(A.dy, A.os[l], g(pre + "self_out.weight"), d, d, R, a_layout=MN, b_layout=MN, lda=d, ldb=d)
-            native.colsum(A.dy, R, d, g(pre + "self_out.bias"), A.cs_ws)
+            dW(A.dy, A.os[l], pre + "self_out.weight", pre + "self_out.bias", d, d, R, d, d)
             native.gemm(A.dy, w(pre + "self_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d)
             qkv = A.qkv[l]
             sa = native.attn_args(qkv, 3 * d, T * 3 * d, qkv[:, d:], 3 * d, T * 3 * d, qkv[:, 2 * d:], 3 * d, T * 3 * d,
@@ -373,16 +380,13 @@ class TransformerDecoder:
             sg = native.attn_grads(A.do, d, T * d, A.dqkv, 3 * d, T * 3 * d, A.dqkv[:, d:], 3 * d, T * 3 * d,
                                    A.dqkv[:, 2 * d:], 3 * d, T * 3 * d, A.delta)
             native.attention_bwd(native.dtype_code(A.dq), B, H, T, T, sa, sg)
-            native.gemm(A.dqkv, xin, g(pre + "self_in.weight"), 3 * d, d, R, a_layout=MN, b_layout=MN, lda=3 * d, ldb=d)
-            native.colsum(A.dqkv, R, 3 * d, g(pre + "self_in.bias"), A.cs_ws)
+            dW(A.dqkv, xin, pre + "self_in.weight", pre + "self_in.bias", 3 * d, d, R, 3 * d, d)
             native.gemm(A.dqkv, w(pre + "self_in.weight"), A.dx, R, d, 3 * d, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
             if grads_ready:
                 grads_ready(pre + "linear2.weight", pre + "norm1.bias")
         # cross K/V of all layers
         BS = B * S
-        native.gemm(A.dkv, mem, g("cross_kv.weight"), L * 2 * d, d, BS, a_layout=MN, b_layout=MN, lda=L * 2 * d,
-                    ldb=mem_ld)
-        native.colsum(A.dkv, BS, L * 2 * d, g("cross_kv.bias"), A.cs_ws)
+        dW(A.dkv, mem, "cross_kv.weight", "cross_kv.bias", L * 2 * d, d, BS, L * 2 * d, mem_ld)
         # embedding (scatter-add into a zeroed table gradient; PAD row gets nothing)
         ge = g("token_embedding.weight")
         native.zero(ge)
@@ -390,10 +394,8 @@ class TransformerDecoder:
         last = "token_embedding.weight"
         if proj_input is not None:
             enc_rows, enc_ld, E = proj_input
-            native.gemm(A.dkv, w("cross_kv.weight"), A.dmem, BS, d, L * 2 * d, b_layout=MN, ldb=d)
-            native.gemm(A.dmem, enc_rows, g("projection.weight"), d, E, BS, a_layout=MN, b_layout=MN, lda=d,
-                        ldb=enc_ld)
-            native.colsum(A.dmem, BS, d, g("projection.bias"), A.cs_ws)
+            native.gemm(A.dkv, w("cross_kv.weight"), A.dmem, BS, d, L * 2 * d, b_layout=MN, ldb=d, workspace=ws)
+            dW(A.dmem, enc_rows, "projection.weight", "projection.bias", d, E, BS, d, enc_ld)
             last = "projection.bias"
         if grads_ready:
             grads_ready("cross_kv.weight", last)

@@ -41,7 +41,7 @@ class GemmArgs(ctypes.Structure):
                 ("A", vp), ("lda", L), ("B", vp), ("ldb", L), ("C", vp), ("ldc", L), ("alpha", Fl),
                 ("bias", vp), ("act", I), ("residual", vp), ("ldr", L), ("aux", vp), ("ld_aux", L),
                 ("aux_scale", Fl), ("drop_p", Fl), ("seed", vp), ("site", U32), ("out_f32", I),
-                ("accumulate", I)]
+                ("accumulate", I), ("rowsum", vp), ("workspace", vp), ("workspace_bytes", L)]
 
 
 class AttnArgs(ctypes.Structure):
@@ -62,6 +62,7 @@ SIGNATURES = {
     "mit_last_error": (ctypes.c_char_p, []),
     "mit_abi_version": (I, []),
     "mit_gemm": (I, [ctypes.POINTER(GemmArgs), vp]),
+    "mit_gemm_workspace_bytes": (L, [L, L, L]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
@@ -140,8 +141,9 @@ def dtype_code(t: torch.Tensor) -> int:
 # ------------------------------------------------------------------------------------------------
 def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ldb=None, ldc=None, bias=None,
          act=ACT_NONE, residual=None, ldr=None, aux=None, ld_aux=None, aux_scale=1.0, alpha=1.0, drop_p=0.0,
-         seed=None, site=0, accumulate=False):
-    """C = epi(alpha * A(m,k) B(k,n)); see include/mit_hip.h. Output dtype = C.dtype (f32 or operand dtype)."""
+         seed=None, site=0, accumulate=False, rowsum=None, workspace=None):
+    """C = epi(alpha * A(m,k) B(k,n)); see include/mit_hip.h. Output dtype = C.dtype (f32 or operand dtype).
+    rowsum: optional f32 [M] <- sum_k A(m,k) (fused bias gradient); workspace: split-K scratch."""
     dt = dtype_code(A)
     if B.dtype != A.dtype:
         raise NativeError("gemm: A and B dtypes differ")
@@ -156,7 +158,8 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
         ldc = N
     g = GemmArgs(dt, a_layout, b_layout, M, N, K, ptr(A), lda, ptr(B), ldb, ptr(C), ldc, alpha, ptr(bias), act,
                  ptr(residual), ldr if ldr is not None else ldc, ptr(aux), ld_aux if ld_aux is not None else ldc,
-                 aux_scale, drop_p, ptr(seed), site, out_f32, 1 if accumulate else 0)
+                 aux_scale, drop_p, ptr(seed), site, out_f32, 1 if accumulate else 0, ptr(rowsum), ptr(workspace),
+                 0 if workspace is None else workspace.numel() * workspace.element_size())
     probe = _gemm_probe
     if probe is not None:
         probe.before(dt, a_layout, b_layout, M, N, K)
@@ -173,6 +176,10 @@ def set_gemm_probe(probe):
     every GEMM launch (bench.py records HIP events there to time the GEMM kernels in place)."""
     global _gemm_probe
     _gemm_probe = probe
+
+
+def gemm_workspace_bytes(M, N, K):
+    return lib().mit_gemm_workspace_bytes(M, N, K)
 
 
 def linear(x, w, out, *, bias=None, act=ACT_NONE, residual=None, drop_p=0.0, seed=None, site=0):
