@@ -122,6 +122,8 @@ def compare_stat(prefix, name, t, tensors, meta, rtol, atol, scale_tol=0.0):
         if m is not None:
             keep = keep[m[idx]]
         got, ref = got[keep], ref[keep]
+    if got.numel() == 0:
+        return 0.0
     torch.testing.assert_close(got, ref, rtol=rtol, atol=atol, msg=lambda s: f"{prefix} {name}: {s}")
     st = tensors[f"{prefix}.stats.{name}"].double()
     flat = t.flatten().double()
