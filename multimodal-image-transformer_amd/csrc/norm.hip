@@ -1,56 +1,117 @@
 // LayerNorm forward/backward, one wave per row, fp32 statistics.
 // Forward fuses the post-LN residual block of torch/nn/modules/transformer.py:1144-1153:
-// z = x + dropout(r); y = (z - mean) * rstd * gamma + beta.
+//   z = x + dropout(r); y = (z - mean) * rstd * gamma + beta.
+// Rows are read as 4-element vectors (8 B bf16 / 16 B f32 per lane) when cols % 256 == 0
+// (512, 768, 1024 — every production width), else element by element.
+// Backward: dz = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma; dgamma/dbeta are
+// reduced in two stages (16-row block partials in registers + LDS, then a column-parallel pass).
 #include "common.h"
 
 namespace {
-constexpr int MAXV_ALL = 32;  // cols <= 64 * 32 = 2048 (per-lane register arrays sized by template)
+constexpr int MAXV_ALL = 32;  // cols <= 64 * 32 = 2048
 
-template <typename T, int MAXV>
+template <typename T>
+struct Vec4;
+template <>
+struct Vec4<bf16> {
+  typedef __attribute__((ext_vector_type(4))) __bf16 type;
+};
+template <>
+struct Vec4<float> {
+  typedef f32x4 type;
+};
+
+template <typename T>
+__device__ __forceinline__ void ld4(const T* p, float* v) {
+  const typename Vec4<T>::type x = *(const typename Vec4<T>::type*)p;
+  v[0] = (float)x[0];
+  v[1] = (float)x[1];
+  v[2] = (float)x[2];
+  v[3] = (float)x[3];
+}
+template <typename T>
+__device__ __forceinline__ void st4(T* p, const float* v) {
+  typename Vec4<T>::type x;
+  x[0] = (T)v[0];
+  x[1] = (T)v[1];
+  x[2] = (T)v[2];
+  x[3] = (T)v[3];
+  *(typename Vec4<T>::type*)p = x;
+}
+
+// element (lane, i, k) of a row: column = (i * 64 + lane) * 4 + k   when VEC; lane + 64 * i otherwise
+template <bool VEC>
+__device__ __forceinline__ long colof(int lane, int i, int k) {
+  return VEC ? (long)(i * 64 + lane) * 4 + k : (long)lane + 64 * i;
+}
+
+template <typename T, int NV, bool VEC>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(long rows, long cols, const T* __restrict__ x, long ldx,
                                                      const T* __restrict__ r, long ldr, const uint64_t* seed,
                                                      uint32_t site, uint32_t thresh, float dscale, int dropout,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      float eps, T* z, T* y, long ldy, float* mean, float* rstd) {
+  constexpr int E = VEC ? 4 : 1;  // elements per (lane, i)
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const uint64_t key = dropout ? site_key(seed, site) : 0ull;
-  float v[MAXV];
+  float v[NV][E];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const long c = lane + 64 * i;
-    float a = 0.f;
-    if (c < cols) {
-      a = to_f(x[row * ldx + c]);
-      if (r) {
-        float b = to_f(r[row * ldr + c]);
-        if (dropout) b *= drop_mul(key, (uint64_t)row * (uint64_t)cols + c, thresh, dscale);
-        a += b;
-      }
+  for (int i = 0; i < NV; ++i) {
+    const long c0 = colof<VEC>(lane, i, 0);
+    if (c0 >= cols) {
+#pragma unroll
+      for (int k = 0; k < E; ++k) v[i][k] = 0.f;
+      continue;
     }
-    v[i] = a;
-    s += a;
+    float a[E], b[E];
+    if (VEC) {
+      ld4(x + row * ldx + c0, a);
+      if (r) ld4(r + row * ldr + c0, b);
+    } else {
+      a[0] = to_f(x[row * ldx + c0]);
+      if (r) b[0] = to_f(r[row * ldr + c0]);
+    }
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      if (r) {
+        if (dropout) b[k] *= drop_mul(key, (uint64_t)row * (uint64_t)cols + c0 + k, thresh, dscale);
+        a[k] += b[k];
+      }
+      v[i][k] = a[k];
+      s += a[k];
+    }
   }
   const float mu = wave_sum(s) / (float)cols;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const long c = lane + 64 * i;
-    if (c < cols) {
-      const float dd = v[i] - mu;
-      q += dd * dd;
+  for (int i = 0; i < NV; ++i)
+    if (colof<VEC>(lane, i, 0) < cols) {
+#pragma unroll
+      for (int k = 0; k < E; ++k) {
+        const float dd = v[i][k] - mu;
+        q += dd * dd;
+      }
     }
-  }
   const float var = wave_sum(q) / (float)cols;
   const float rs = rsqrtf(var + eps);
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const long c = lane + 64 * i;
-    if (c < cols) {
-      if (z) z[row * cols + c] = from_f<T>(v[i]);
-      y[row * ldy + c] = from_f<T>((v[i] - mu) * rs * gamma[c] + beta[c]);
+  for (int i = 0; i < NV; ++i) {
+    const long c0 = colof<VEC>(lane, i, 0);
+    if (c0 >= cols) continue;
+    float o[E];
+    if (VEC) {
+      const f32x4 g4 = *(const f32x4*)(gamma + c0), b4 = *(const f32x4*)(beta + c0);
+#pragma unroll
+      for (int k = 0; k < E; ++k) o[k] = (v[i][k] - mu) * rs * g4[k] + b4[k];
+      if (z) st4(z + row * cols + c0, v[i]);
+      st4(y + row * ldy + c0, o);
+    } else {
+      o[0] = (v[i][0] - mu) * rs * gamma[c0] + beta[c0];
+      if (z) z[row * cols + c0] = from_f<T>(v[i][0]);
+      y[row * ldy + c0] = from_f<T>(o[0]);
     }
   }
   if (lane == 0) {
@@ -59,73 +120,102 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(long rows, long cols, const
   }
 }
 
-constexpr int BWD_ROWS = 32;  // rows per block in the backward (4 waves x 8 rows)
+constexpr int BWD_ROWS = 16;  // rows per block in the backward (4 waves x 4 rows)
 
-template <typename T, int MAXV>
+template <typename T, int NV, bool VEC>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(long rows, long cols, const T* __restrict__ dy,
                                                      const T* __restrict__ z, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                      T* dx, T* dr, const uint64_t* seed, uint32_t site, uint32_t thresh,
                                                      float dscale, int dropout, float* ws) {
-  __shared__ float red[4][2][64 * 4];  // per-wave partials for up to 256 columns per pass
+  constexpr int E = VEC ? 4 : 1;
+  __shared__ float red[4][2][256];  // per-wave column partials, 256 columns per pass
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t key = dropout ? site_key(seed, site) : 0ull;
-  float pg[MAXV], pb[MAXV];
+  float pg[NV][E], pb[NV][E];
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) pg[i] = pb[i] = 0.f;
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < E; ++k) pg[i][k] = pb[i][k] = 0.f;
   const long r0 = (long)blockIdx.x * BWD_ROWS;
   for (int rr = w; rr < BWD_ROWS; rr += 4) {
     const long row = r0 + rr;
     if (row >= rows) break;
     const float mu = mean[row], rs = rstd[row];
-    float g[MAXV], xh[MAXV];
+    float g[NV][E], xh[NV][E];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const long c = lane + 64 * i;
-      g[i] = xh[i] = 0.f;
-      if (c < cols) {
-        const float d = to_f(dy[row * cols + c]);
-        xh[i] = (to_f(z[row * cols + c]) - mu) * rs;
-        g[i] = d * gamma[c];
-        pg[i] += d * xh[i];
-        pb[i] += d;
-        s1 += g[i];
-        s2 += g[i] * xh[i];
+    for (int i = 0; i < NV; ++i) {
+      const long c0 = colof<VEC>(lane, i, 0);
+      float d[E], zz[E], ga[E];
+      if (c0 < cols) {
+        if (VEC) {
+          ld4(dy + row * cols + c0, d);
+          ld4(z + row * cols + c0, zz);
+          const f32x4 g4 = *(const f32x4*)(gamma + c0);
+#pragma unroll
+          for (int k = 0; k < E; ++k) ga[k] = g4[k];
+        } else {
+          d[0] = to_f(dy[row * cols + c0]);
+          zz[0] = to_f(z[row * cols + c0]);
+          ga[0] = gamma[c0];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < E; ++k) d[k] = zz[k] = ga[k] = 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < E; ++k) {
+        xh[i][k] = (c0 < cols) ? (zz[k] - mu) * rs : 0.f;
+        g[i][k] = d[k] * ga[k];
+        pg[i][k] += d[k] * xh[i][k];
+        pb[i][k] += d[k];
+        s1 += g[i][k];
+        s2 += g[i][k] * xh[i][k];
       }
     }
     s1 = wave_sum(s1) / (float)cols;
     s2 = wave_sum(s2) / (float)cols;
 #pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      const long c = lane + 64 * i;
-      if (c < cols) {
-        const float d = rs * (g[i] - s1 - xh[i] * s2);
-        dx[row * cols + c] = from_f<T>(d);
-        if (dr) {
-          const float m = dropout ? drop_mul(key, (uint64_t)row * (uint64_t)cols + c, thresh, dscale) : 1.0f;
-          dr[row * cols + c] = from_f<T>(d * m);
-        }
+    for (int i = 0; i < NV; ++i) {
+      const long c0 = colof<VEC>(lane, i, 0);
+      if (c0 >= cols) continue;
+      float o[E], om[E];
+#pragma unroll
+      for (int k = 0; k < E; ++k) {
+        o[k] = rs * (g[i][k] - s1 - xh[i][k] * s2);
+        om[k] = dropout ? o[k] * drop_mul(key, (uint64_t)row * (uint64_t)cols + c0 + k, thresh, dscale) : o[k];
+      }
+      if (VEC) {
+        st4(dx + row * cols + c0, o);
+        if (dr) st4(dr + row * cols + c0, om);
+      } else {
+        dx[row * cols + c0] = from_f<T>(o[0]);
+        if (dr) dr[row * cols + c0] = from_f<T>(om[0]);
       }
     }
   }
-  // reduce the 4 waves' column partials, 4 column-groups of 64 at a time
+  // reduce the 4 waves' column partials (one (lane, i) slot = E columns); 256 columns per pass
+  constexpr int SLOTS_PER_PASS = 256 / (64 * E);  // i-values per pass
 #pragma unroll
-  for (int base = 0; base < MAXV; base += 4) {
-    if (base * 64 >= cols) continue;  // uniform
+  for (int base = 0; base < NV; base += SLOTS_PER_PASS) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      red[w][0][k * 64 + lane] = (base + k < MAXV) ? pg[(base + k) < MAXV ? base + k : 0] : 0.f;
-      red[w][1][k * 64 + lane] = (base + k < MAXV) ? pb[(base + k) < MAXV ? base + k : 0] : 0.f;
-    }
+    for (int s = 0; s < SLOTS_PER_PASS; ++s)
+#pragma unroll
+      for (int k = 0; k < E; ++k) {
+        const int li = (base + s < NV) ? base + s : 0;
+        const int slot = (s * 64 + lane) * E + k;
+        red[w][0][slot] = (base + s < NV) ? pg[li][k] : 0.f;
+        red[w][1][slot] = (base + s < NV) ? pb[li][k] : 0.f;
+      }
     __syncthreads();
-    // 256 threads: thread t -> column group (t>>6), lane column
     {
-      const int k = threadIdx.x >> 6;
-      const long c = (long)(base + k) * 64 + lane;
-      if (c < cols) {
-        float a = red[0][0][k * 64 + lane] + red[1][0][k * 64 + lane] + red[2][0][k * 64 + lane] + red[3][0][k * 64 + lane];
-        float b = red[0][1][k * 64 + lane] + red[1][1][k * 64 + lane] + red[2][1][k * 64 + lane] + red[3][1][k * 64 + lane];
+      const int slot = threadIdx.x;  // 0..255 -> (s, lane, k)
+      const int k = slot % E, l2 = (slot / E) % 64, s = slot / (64 * E);
+      const long c = colof<VEC>(l2, base + s, k);
+      if (base + s < NV && c < cols) {
+        const float a = red[0][0][slot] + red[1][0][slot] + red[2][0][slot] + red[3][0][slot];
+        const float b = red[0][1][slot] + red[1][1][slot] + red[2][1][slot] + red[3][1][slot];
         ws[(long)blockIdx.x * 2 * cols + c] = a;
         ws[(long)blockIdx.x * 2 * cols + cols + c] = b;
       }
@@ -134,13 +224,41 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long rows, long cols, const
   }
 }
 
-__global__ void ln_param_reduce(long nblk, long cols, const float* __restrict__ ws, float* dgamma, float* dbeta) {
-  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * cols) return;
+// column-parallel sum of the block partials: 64 columns x 4 strided partial-row groups per block
+__global__ __launch_bounds__(256) void ln_param_reduce(long nblk, long cols, const float* __restrict__ ws,
+                                                       float* dgamma, float* dbeta) {
+  __shared__ float part[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const long c = (long)blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (long b = 0; b < nblk; ++b) s += ws[b * 2 * cols + c];
-  if (c < cols) dgamma[c] = s;
-  else dbeta[c - cols] = s;
+  if (c < 2 * cols) {
+    long b = grp;
+    for (; b + 12 < nblk; b += 16) {
+      s += ws[b * 2 * cols + c] + ws[(b + 4) * 2 * cols + c] + ws[(b + 8) * 2 * cols + c] +
+           ws[(b + 12) * 2 * cols + c];
+    }
+    for (; b < nblk; b += 4) s += ws[b * 2 * cols + c];
+  }
+  part[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && c < 2 * cols) {
+    const float t = part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl];
+    if (c < cols) dgamma[c] = t;
+    else dbeta[c - cols] = t;
+  }
+}
+
+template <typename T, bool VEC, typename F>
+void dispatch_nv(long cols, F&& f) {
+  const long per = VEC ? 256 : 64;
+  const long nv = (cols + per - 1) / per;
+  if (nv <= 1) f(std::integral_constant<int, 1>());
+  else if (nv <= 2) f(std::integral_constant<int, 2>());
+  else if (nv <= 3) f(std::integral_constant<int, 3>());
+  else if (nv <= 4) f(std::integral_constant<int, 4>());
+  else if (nv <= 8) f(std::integral_constant<int, 8>());
+  else if (nv <= 16) f(std::integral_constant<int, 16>());
+  else f(std::integral_constant<int, 32>());
 }
 }  // namespace
 
@@ -155,20 +273,29 @@ extern "C" int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x,
   const int dropout = (r != nullptr) && r_drop_p > 0.f;
   const uint32_t th = drop_threshold(r_drop_p);
   const float sc = r_drop_p < 1.f ? 1.f / (1.f - r_drop_p) : 0.f;
+  const size_t esz = dtype == MIT_BF16 ? 2 : 4;
+  const bool vec = cols % 256 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (!r || ldr % 4 == 0) &&
+                   ((uintptr_t)x % (4 * esz)) == 0 && ((uintptr_t)y % (4 * esz)) == 0 &&
+                   (!r || ((uintptr_t)r % (4 * esz)) == 0) && (!z || ((uintptr_t)z % (4 * esz)) == 0) &&
+                   ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0;
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
-#define LNF(T, NV)                                                                                              \
-  hipLaunchKernelGGL((ln_fwd_kernel<T, NV>), grid, dim3(256), 0, s, rows, cols, (const T*)x, ldx, (const T*)r, ldr, \
-                     seed, site, th, sc, dropout, gamma, beta, eps, (T*)z, (T*)y, ldy, mean, rstd)
-#define LNF_DT(T)                 \
-  if (cols <= 128) LNF(T, 2);     \
-  else if (cols <= 256) LNF(T, 4); \
-  else if (cols <= 512) LNF(T, 8); \
-  else if (cols <= 1024) LNF(T, 16); \
-  else LNF(T, 32);
-  if (dtype == MIT_BF16) { LNF_DT(bf16) } else { LNF_DT(float) }
-#undef LNF_DT
-#undef LNF
+  auto go = [&](auto tt, auto vv) {
+    typedef decltype(tt) T;
+    constexpr bool V = decltype(vv)::value;
+    dispatch_nv<T, V>(cols, [&](auto nv) {
+      constexpr int NV = decltype(nv)::value;
+      hipLaunchKernelGGL((ln_fwd_kernel<T, NV, V>), grid, dim3(256), 0, s, rows, cols, (const T*)x, ldx, (const T*)r,
+                         ldr, seed, site, th, sc, dropout, gamma, beta, eps, (T*)z, (T*)y, ldy, mean, rstd);
+    });
+  };
+  if (dtype == MIT_BF16) {
+    if (vec) go(bf16(), std::true_type());
+    else go(bf16(), std::false_type());
+  } else {
+    if (vec) go(float(), std::true_type());
+    else go(float(), std::false_type());
+  }
   MIT_LAUNCH_CHECK("mit_layernorm_fwd");
   return MIT_OK;
 }
@@ -188,21 +315,29 @@ extern "C" int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy
   const uint32_t th = drop_threshold(r_drop_p);
   const float sc = r_drop_p < 1.f ? 1.f / (1.f - r_drop_p) : 0.f;
   const long nblk = (rows + BWD_ROWS - 1) / BWD_ROWS;
+  const size_t esz = dtype == MIT_BF16 ? 2 : 4;
+  const bool vec = cols % 256 == 0 && ((uintptr_t)dy % (4 * esz)) == 0 && ((uintptr_t)z % (4 * esz)) == 0 &&
+                   ((uintptr_t)dx % (4 * esz)) == 0 && (!dr || ((uintptr_t)dr % (4 * esz)) == 0) &&
+                   ((uintptr_t)gamma % 16) == 0;
   hipStream_t s = (hipStream_t)stream;
-#define LNB(T, NV)                                                                                          \
-  hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3((unsigned)nblk), dim3(256), 0, s, rows, cols, (const T*)dy, \
-                     (const T*)z, mean, rstd, gamma, (T*)dx, (T*)dr, seed, site, th, sc, dropout, ws)
-#define LNB_DT(T)                 \
-  if (cols <= 128) LNB(T, 2);     \
-  else if (cols <= 256) LNB(T, 4); \
-  else if (cols <= 512) LNB(T, 8); \
-  else if (cols <= 1024) LNB(T, 16); \
-  else LNB(T, 32);
-  if (dtype == MIT_BF16) { LNB_DT(bf16) } else { LNB_DT(float) }
-#undef LNB_DT
-#undef LNB
+  auto go = [&](auto tt, auto vv) {
+    typedef decltype(tt) T;
+    constexpr bool V = decltype(vv)::value;
+    dispatch_nv<T, V>(cols, [&](auto nv) {
+      constexpr int NV = decltype(nv)::value;
+      hipLaunchKernelGGL((ln_bwd_kernel<T, NV, V>), dim3((unsigned)nblk), dim3(256), 0, s, rows, cols, (const T*)dy,
+                         (const T*)z, mean, rstd, gamma, (T*)dx, (T*)dr, seed, site, th, sc, dropout, ws);
+    });
+  };
+  if (dtype == MIT_BF16) {
+    if (vec) go(bf16(), std::true_type());
+    else go(bf16(), std::false_type());
+  } else {
+    if (vec) go(float(), std::true_type());
+    else go(float(), std::false_type());
+  }
   MIT_LAUNCH_CHECK("mit_layernorm_bwd");
-  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((2 * cols + 255) / 256)), dim3(256), 0, s, nblk, cols, ws, dgamma,
+  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((2 * cols + 63) / 64)), dim3(256), 0, s, nblk, cols, ws, dgamma,
                      dbeta);
   MIT_LAUNCH_CHECK("mit_layernorm_bwd(reduce)");
   return MIT_OK;

@@ -87,7 +87,7 @@ def degenerate_mask(name: str, t: torch.Tensor, meta=None):
     return None
 
 
-def compare_stat(prefix, name, t, tensors, meta, rtol, atol, scale_tol=0.0):
+def compare_stat(prefix, name, t, tensors, meta, rtol, atol, scale_tol=0.0, outlier_frac=0.0):
     """Compare a tensor to its fixture entry (full / sample+stats). Returns max abs err on samples.
     scale_tol: absolute tolerance as a fraction of the tensor's max |value| (sum-order noise of
     reductions is relative to the tensor's scale, not to each element)."""
@@ -109,7 +109,10 @@ def compare_stat(prefix, name, t, tensors, meta, rtol, atol, scale_tol=0.0):
             m = gm if m is None else (m & gm)
         if m is not None:
             got, ref = got.flatten()[m], ref.flatten()[m]
-        torch.testing.assert_close(got, ref, rtol=rtol, atol=atol, msg=lambda s: f"{prefix} {name}: {s}")
+        if outlier_frac:
+            _assert_close_outliers(got.flatten(), ref.flatten(), rtol, atol, outlier_frac, 10 * atol, f"{prefix} {name}")
+        else:
+            torch.testing.assert_close(got, ref, rtol=rtol, atol=atol, msg=lambda s: f"{prefix} {name}: {s}")
         return float((got - ref).abs().max())
     idx = torch.tensor(meta["sample_index"][name])
     ref = tensors[f"{prefix}.sample.{name}"]
@@ -131,3 +134,16 @@ def compare_stat(prefix, name, t, tensors, meta, rtol, atol, scale_tol=0.0):
     if m is None:
         assert abs(norm - st[1]) <= rtol * abs(st[1]) + atol * flat.numel() ** 0.5, f"{prefix} {name} norm"
     return float((got - ref).abs().max())
+
+
+def _assert_close_outliers(got, ref, rtol, atol, outlier_frac, outlier_atol, what):
+    """assert_close that tolerates up to `outlier_frac` of elements beyond tolerance, each still
+    within `outlier_atol` (ReLU-boundary flips: a pre-activation within an ulp of 0 gets a
+    different mask under another summation order, moving one row's contribution)."""
+    bad = (got - ref).abs() > atol + rtol * ref.abs()
+    nbad = int(bad.sum())
+    if nbad == 0:
+        return
+    assert nbad <= max(1, int(outlier_frac * got.numel())), f"{what}: {nbad}/{got.numel()} elements off"
+    worst = float((got - ref)[bad].abs().max())
+    assert worst <= outlier_atol, f"{what}: outlier error {worst:.3e} > {outlier_atol:.3e}"

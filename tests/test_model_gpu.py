@@ -102,7 +102,8 @@ def test_train_steps_fp32_match_reference(name):
         grads["projection.bias"] = m.store.g("projection.bias").clone()
     after = m.state_dict()
     for k in names:
-        FX.compare_stat("grad1", k, grads[k].cpu() * coef, T, meta, rtol=2e-3, atol=2e-6, scale_tol=1e-3)
+        FX.compare_stat("grad1", k, grads[k].cpu() * coef, T, meta, rtol=2e-3, atol=2e-6, scale_tol=1e-3,
+                        outlier_frac=2e-3)
         FX.compare_stat("delta1", k, (after[k] - before[k]).cpu(), T, meta, rtol=2e-3, atol=2e-6)
     if meta["steps"] > 1:
         losses = []
