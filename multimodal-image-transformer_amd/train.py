@@ -1,0 +1,148 @@
+"""Training loop surface of the reference train.py, on the fused MI355X train step.
+
+``train_one_epoch`` / ``evaluate`` keep the reference signatures (train.py:62, 125) and semantics:
+per batch zero_grad -> forward -> CE(ignore PAD) -> backward -> clip_grad_norm_(grad_clip_value)
+-> optimizer.step() -> scheduler.step(); the epoch returns the mean batch loss. Differences that
+are deliberate:
+  * forward + loss + backward are ONE kernel sequence (model.train_step) and clip + AdamW one more
+    (optim.AdamW.step); ``criterion`` is accepted for signature compatibility — the loss is
+    always CrossEntropyLoss(ignore_index=PAD) as train.py:327 constructs it;
+  * the per-batch loss stays on the device; the reference's per-step ``loss.item()`` sync
+    (train.py:109) becomes one sync per ``log_interval`` batches and one at the end of the epoch.
+``main()`` runs the loop on synthetic batches (the dataset / tokenizer / W&B / Hub plumbing of the
+reference main() is out of scope: SURVEY.md §2a) and writes reference-format checkpoints.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import time
+
+import torch
+
+import config
+import optim
+from model import ImageToTextModel
+
+
+def _lr_of(optimizer):
+    return optimizer.param_groups[0]["lr"]
+
+
+def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_value, scheduler, epoch,
+                    log_interval, wandb_run, dist=None):
+    """train.py:62-123 on the fused step. Returns the average training loss of the epoch."""
+    model.train()
+    total = torch.zeros(1, dtype=torch.float32, device=model.device)
+    n = 0
+    for i, batch in enumerate(dataloader):
+        optimizer.zero_grad()
+        loss = model.train_step(batch["images"], batch["decoder_input_tokens"], batch["target_tokens"], dist=dist)
+        optimizer.step(grad_clip_value if grad_clip_value > 0 else 0.0)
+        if scheduler:
+            scheduler.step()
+        total += loss
+        n += 1
+        if log_interval and (i + 1) % log_interval == 0:
+            lv = loss.item()
+            print(f"epoch {epoch + 1} batch {i + 1}: loss {lv:.4f} lr {_lr_of(optimizer):.2e}", flush=True)
+            if wandb_run:
+                wandb_run.log({"train_batch_loss": lv, "learning_rate": _lr_of(optimizer),
+                               "global_step": epoch * max(1, len(dataloader)) + i + 1})
+    return (total / max(n, 1)).item()
+
+
+@torch.no_grad()
+def evaluate(model, dataloader, criterion, device):
+    """train.py:125-151: mean over batches of CE(ignore PAD), no dropout."""
+    model.eval()
+    total = torch.zeros(1, dtype=torch.float32, device=model.device)
+    n = 0
+    for batch in dataloader:
+        total += model.eval_loss(batch["images"], batch["decoder_input_tokens"], batch["target_tokens"])
+        n += 1
+    model.train()
+    return (total / max(n, 1)).item()
+
+
+class LinearWarmup:
+    """transformers.get_linear_schedule_with_warmup semantics (train.py:331-341)."""
+
+    def __init__(self, optimizer, num_warmup_steps, num_training_steps):
+        self.opt, self.w, self.t, self.step_n = optimizer, num_warmup_steps, num_training_steps, 0
+        self.base = _lr_of(optimizer)
+        self._apply()
+
+    def _factor(self):
+        s = self.step_n
+        if s < self.w:
+            return s / max(1, self.w)
+        return max(0.0, (self.t - s) / max(1, self.t - self.w))
+
+    def _apply(self):
+        self.opt.param_groups[0]["lr"] = self.base * self._factor()
+
+    def step(self):
+        self.step_n += 1
+        self._apply()
+
+    def get_last_lr(self):
+        return [_lr_of(self.opt)]
+
+
+def synthetic_loader(n_batches, B, seq_len, vocab, image, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n_batches):
+        cap = torch.randint(4, vocab, (B, seq_len), generator=g)
+        cap[:, 0] = config.START_TOKEN_ID
+        out.append({"images": torch.randn(B, 3, image, image, generator=g),
+                    "decoder_input_tokens": cap[:, :-1], "target_tokens": cap[:, 1:]})
+    return out
+
+
+def save_checkpoint(model, optimizer, epoch, val_loss, path_prefix):
+    """train.py:412-442: a .pt dict {epoch, model_state_dict, optimizer_state_dict, best_val_loss}
+    and a .safetensors of model.state_dict() (reference key names)."""
+    from safetensors.torch import save_file
+    name = f"{path_prefix}_{config.ENCODER_MODEL_NAME.replace('/', '_')}_epoch_{epoch + 1}_val_loss_{val_loss:.4f}"
+    sd = {k: v.detach().cpu().contiguous() for k, v in model.state_dict().items()}
+    torch.save({"epoch": epoch, "model_state_dict": sd, "optimizer_state_dict": optimizer.state_dict(),
+                "best_val_loss": val_loss}, name + ".pt")
+    save_file(sd, name + ".safetensors")
+    return name
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Train the captioning model on synthetic batches (MI355X path)")
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--batches", type=int, default=20)
+    ap.add_argument("--batch-size", type=int, default=config.BATCH_SIZE)
+    ap.add_argument("--seq-len", type=int, default=64)
+    ap.add_argument("--out", default=None, help="checkpoint prefix (optional)")
+    args = ap.parse_args(argv)
+    torch.manual_seed(config.RANDOM_SEED)
+    model = ImageToTextModel(config.VOCAB_SIZE, config.DECODER_EMBED_DIM, config.DECODER_HEADS, config.DECODER_LAYERS,
+                             config.DECODER_FF_DIM, config.MAX_SEQ_LEN, config.DECODER_DROPOUT, config.PAD_TOKEN_ID)
+    opt = optim.AdamW(model.store, lr=config.LEARNING_RATE, betas=(config.ADAM_BETA1, config.ADAM_BETA2),
+                      eps=config.ADAM_EPS, weight_decay=config.WEIGHT_DECAY)
+    sched = None
+    if config.WARMUP_STEPS > 0:
+        sched = LinearWarmup(opt, config.WARMUP_STEPS, args.batches * args.epochs)
+    train = synthetic_loader(args.batches, args.batch_size, args.seq_len, config.VOCAB_SIZE, model.encoder.image, 1)
+    val = synthetic_loader(2, args.batch_size, args.seq_len, config.VOCAB_SIZE, model.encoder.image, 2)
+    best = math.inf
+    for epoch in range(args.epochs):
+        t0 = time.time()
+        tl = train_one_epoch(model, train, opt, None, "cuda", config.GRAD_CLIP_VALUE, sched, epoch, config.LOG_INTERVAL,
+                             None)
+        vl = evaluate(model, val, None, "cuda")
+        print(f"epoch {epoch + 1}: train {tl:.4f} val {vl:.4f} ({time.time() - t0:.1f}s)", flush=True)
+        if vl < best and args.out:
+            best = vl
+            print("saved", save_checkpoint(model, opt, epoch, vl, args.out))
+
+
+if __name__ == "__main__":
+    main()

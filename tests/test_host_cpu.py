@@ -63,3 +63,26 @@ def test_cfg1_flop_accounting_matches_survey():
         return L * layer + 2 * T * d * V + 2 * S * E * d
     assert abs((enc + 3 * dec(197)) / 1e9 - 50.17) < 0.05
     assert abs((enc + 3 * dec(1)) / 1e9 - 45.56) < 0.05
+
+
+def test_utils_masks_match_reference_semantics():
+    import utils
+    m = utils.generate_square_subsequent_mask(4)
+    assert m[0, 1] == float("-inf") and m[1, 0] == 0 and m[3, 3] == 0
+    tok = torch.tensor([[2, 5, 0, 0]])
+    assert utils.create_padding_mask(tok, 0).tolist() == [[False, False, True, True]]
+
+
+def test_linear_warmup_schedule():
+    import train
+
+    class O:
+        param_groups = [{"lr": 1.0}]
+    o = O()
+    s = train.LinearWarmup(o, 2, 10)
+    assert o.param_groups[0]["lr"] == 0.0
+    s.step()
+    assert abs(o.param_groups[0]["lr"] - 0.5) < 1e-9
+    for _ in range(9):
+        s.step()
+    assert o.param_groups[0]["lr"] == 0.0
