@@ -20,6 +20,8 @@
 //     writes 16 bytes (coalesced rows instead of the MFMA layout's 4-row x 16-column scatter).
 //   * tile order: XCD-aware remap + 8-row grouping so tiles sharing A/B panels share an L2.
 // fp32 path (parity mode): a plain LDS-tiled FMA kernel with the identical epilogue semantics.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -163,6 +165,34 @@ struct Stage {
   }
 };
 
+// LDS-DMA fill of one 16 KiB operand tile: 1024 16-B chunks = 16 wave-instructions, wave w issues
+// w*4 .. w*4+3. The DMA writes each instruction's 1 KiB linearly (base + lane*16), so the swizzle is
+// applied to the SOURCE address instead: linear position p holds logical chunk phys ^ swizzle(row)
+// (the XOR is an involution), which reproduces exactly the koff / mnoff images read by frag().
+template <int LAY>
+__device__ __forceinline__ void glds_tile(__amdgpu_buffer_rsrc_t rs, char* tile, long ld, long rows_total, long K,
+                                          long row0, long k0, int w, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int inst = w * 4 + j;
+    const int id = inst * 64 + lane;
+    bool ok;
+    long off;
+    if (LAY == MIT_K_CONTIG) {
+      const int r = id >> 3, c = (id & 7) ^ ((r >> 1) & 7);
+      ok = (row0 + r < rows_total) && (k0 + c * 8 < K);
+      off = (row0 + r) * ld + k0 + c * 8;
+    } else {
+      const int kr = id >> 4, c = (id & 15) ^ (mn_swz(kr) >> 4);
+      ok = (k0 + kr < K) && (row0 + c * 8 < rows_total);
+      off = (k0 + kr) * ld + row0 + c * 8;
+    }
+    const uint32_t boff = ok ? (uint32_t)(off * 2) : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(tile + inst * 1024), 16,
+                                             boff, 0, 0, 0);
+  }
+}
+
 // MFMA operand fragment: rows [rbase, rbase+16) of the tile, k-slice kk (32 wide)
 template <int LAY>
 __device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kk, int lane) {
@@ -181,7 +211,7 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kk, int l
   }
 }
 
-template <int ALAY, int BLAY>
+template <int ALAY, int BLAY, bool GLDS>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                         long M, long N, long K, long lda, long ldb, long ldc,
                                                         int a_bytes, int b_bytes, Epi e, int ksplit, long kchunk,
@@ -234,22 +264,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
   const bf16x2 one2 = {(bf16)1.0f, (bf16)1.0f};
 
-  Stage<ALAY> sa;
-  Stage<BLAY> sb;
   const int nk = (int)((ke - kb + BK - 1) / BK);
-  sa.load(ra, lda, M, ke, m0, kb, tid);
-  sb.load(rb, ldb, N, ke, n0, kb, tid);
-  sa.store(AS(0), tid);
-  sb.store(BS(0), tid);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      sa.load(ra, lda, M, ke, m0, kb + (long)(kt + 1) * BK, tid);
-      sb.load(rb, ldb, N, ke, n0, kb + (long)(kt + 1) * BK, tid);
-    }
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[4], bfr[4];
@@ -271,11 +287,49 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
         }
       }
     }
-    if (more) {
-      sa.store(AS(cur ^ 1), tid);
-      sb.store(BS(cur ^ 1), tid);
+  };
+
+  if constexpr (GLDS) {
+    // direct-to-LDS buffer loads (LDS-DMA): no staging registers, no ds_write pass. Two stages:
+    // the next tile's DMA is in flight while this tile computes; counted vmcnt + raw barriers
+    // (a __syncthreads() would drain the in-flight DMA with vmcnt(0), guide §5).
+    glds_tile<ALAY>(ra, AS(0), lda, M, ke, m0, kb, wid, lane);
+    glds_tile<BLAY>(rb, BS(0), ldb, N, ke, n0, kb, wid, lane);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) {
+        glds_tile<ALAY>(ra, AS(cur ^ 1), lda, M, ke, m0, kb + (long)(kt + 1) * BK, wid, lane);
+        glds_tile<BLAY>(rb, BS(cur ^ 1), ldb, N, ke, n0, kb + (long)(kt + 1) * BK, wid, lane);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this tile's 8 DMAs done, next 8 in flight
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
+      compute(cur);
+      __builtin_amdgcn_s_barrier();  // every wave is done reading buffer cur before it is refilled
     }
+  } else {
+    Stage<ALAY> sa;
+    Stage<BLAY> sb;
+    sa.load(ra, lda, M, ke, m0, kb, tid);
+    sb.load(rb, ldb, N, ke, n0, kb, tid);
+    sa.store(AS(0), tid);
+    sb.store(BS(0), tid);
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nk;
+      if (more) {
+        sa.load(ra, lda, M, ke, m0, kb + (long)(kt + 1) * BK, tid);
+        sb.load(rb, ldb, N, ke, n0, kb + (long)(kt + 1) * BK, tid);
+      }
+      compute(cur);
+      if (more) {
+        sa.store(AS(cur ^ 1), tid);
+        sb.store(BS(cur ^ 1), tid);
+      }
+      __syncthreads();
+    }
   }
 #undef AS
 #undef BS
@@ -440,9 +494,23 @@ template <int AL, int BL>
 void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, int ksplit, long kchunk,
                  hipStream_t s) {
   const long nbm = (g->M + BM - 1) / BM, nbn = (g->N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL>), dim3((unsigned)(nbm * nbn * ksplit)), dim3(256), SMEM_BYTES, s,
-                     (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                     b_bytes, e, ksplit, kchunk, (float*)g->workspace, g->rowsum);
+  static const int glds = getenv("MIT_GEMM_GLDS") ? atoi(getenv("MIT_GEMM_GLDS")) : 1;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<AL, BL, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              SMEM_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<AL, BL, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              SMEM_BYTES);
+    attr = true;
+  }
+  if (glds)
+    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, true>), dim3((unsigned)(nbm * nbn * ksplit)), dim3(256), SMEM_BYTES, s,
+                       (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                       b_bytes, e, ksplit, kchunk, (float*)g->workspace, g->rowsum);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, false>), dim3((unsigned)(nbm * nbn * ksplit)), dim3(256), SMEM_BYTES,
+                       s, (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                       b_bytes, e, ksplit, kchunk, (float*)g->workspace, g->rowsum);
 }
 template <int AL, int BL>
 void launch_f32(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
@@ -455,7 +523,7 @@ inline bool al16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 
 }  // namespace
 
-static bool mit_gemm_smem_set = false;
+
 
 extern "C" long mit_gemm_workspace_bytes(long M, long N, long K) {
   long kc;
@@ -510,13 +578,6 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
           (!g->residual || (g->ldr % 8 == 0 && al16(g->residual))) && (!g->aux || (g->ld_aux % 8 == 0 && al16(g->aux)));
   hipStream_t s = (hipStream_t)stream;
   if (g->dtype == MIT_BF16) {
-    if (!mit_gemm_smem_set) {
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
-      mit_gemm_smem_set = true;
-    }
     const int ab = (int)a_bytes, bb = (int)b_bytes;
     long kchunk = g->K;
     int ks = 1;
