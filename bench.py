@@ -133,6 +133,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
     args = ap.parse_args()
 
     from dist import DataParallel, init_from_env
@@ -146,9 +147,20 @@ def main():
     model.train()
     images, di, tg = synthetic_batch(args.batch, args.seq_len, args.vocab, dev, 1000 + rank)
 
-    def step():
-        model.train_step(images, di, tg, dist=dp)
-        opt.step(5.0)
+    def eager_step():
+        return model.train_step(images, di, tg, dist=dp)
+
+    use_graph = world == 1 and not args.no_graph
+    if use_graph:
+        gstep = model.make_graphed_step(opt, images, di, tg, 5.0)
+
+        def step():
+            return gstep()
+    else:
+        def step():
+            loss = eager_step()
+            opt.step(5.0)
+            return loss
 
     def barrier():
         if world > 1:
@@ -167,7 +179,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = t.item()
-    loss = model.train_step(images, di, tg, dist=dp).item()
+    loss = step().item()
 
     pairs = args.batch * world * args.steps
     value = pairs / elapsed
@@ -188,8 +200,9 @@ def main():
         import native
         probe = GemmProbe()
         native.set_gemm_probe(probe)
-        for _ in range(min(args.steps, 5)):
-            step()
+        for _ in range(min(args.steps, 5)):  # eager replay of the same step (events need eager launches)
+            eager_step()
+            opt.step(5.0)
         native.set_gemm_probe(None)
         agg = probe.summary()
         names = {(0, 0): "gemm_bf16_kernel<0,0> (NT: forward)", (0, 1): "gemm_bf16_kernel<0,1> (NN: dX)",

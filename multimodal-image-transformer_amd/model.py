@@ -60,6 +60,22 @@ class ViTImageProcessorLite:
         return {"pixel_values": torch.stack(out)}
 
 
+class GraphedStep:
+    """A captured train step. step(images, decoder_input_tokens, target_tokens) copies a batch into
+    the static buffers (skip by passing nothing) and replays; returns the loss device scalar."""
+
+    def __init__(self, graph, images, dec_in, targets, loss):
+        self.graph, self.images, self.dec_in, self.targets, self.loss = graph, images, dec_in, targets, loss
+
+    def __call__(self, images=None, decoder_input_tokens=None, target_tokens=None):
+        if images is not None:
+            self.images.copy_(images, non_blocking=True)
+            self.dec_in.copy_(decoder_input_tokens, non_blocking=True)
+            self.targets.copy_(target_tokens, non_blocking=True)
+        self.graph.replay()
+        return self.loss
+
+
 class ImageToTextModel:
     def __init__(self, decoder_vocab_size: int, decoder_embed_dim: int, decoder_heads: int, decoder_layers: int,
                  decoder_ff_dim: int, decoder_max_seq_len: int, decoder_dropout: float, decoder_pad_idx: int, *,
@@ -190,6 +206,37 @@ class ImageToTextModel:
         if dist is not None:
             dist.finish_backward(A.loss)
         return A.loss
+
+    def make_graphed_step(self, optimizer, images, decoder_input_tokens, target_tokens, max_norm: float):
+        """Capture train_step + optimizer.step(max_norm) (train.py:75-100, ~300 kernel launches) into
+        ONE hipGraph over static input buffers. The two warm-up executions that size the arenas
+        are undone (parameters, AdamW state and counters restored) before capture, so the graph
+        starts from the same state the model had. Returns a GraphedStep (call it per batch)."""
+        dev = self.device
+        st_img = images.to(dev).clone()
+        st_in = decoder_input_tokens.to(dev, torch.int64).clone()
+        st_tg = target_tokens.to(dev, torch.int64).clone()
+        store = self.store
+        store.ensure_optimizer_state()
+        saved = [t.clone() for t in (store.master, store.shadow, store.exp_avg, store.exp_avg_sq, optimizer.step_t,
+                                     self.seed_t)]
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self.train_step(st_img, st_in, st_tg)
+                optimizer.step(max_norm)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        for dst, src in zip((store.master, store.shadow, store.exp_avg, store.exp_avg_sq, optimizer.step_t,
+                             self.seed_t), saved):
+            dst.copy_(src)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            loss = self.train_step(st_img, st_in, st_tg)
+            optimizer.step(max_norm)
+        return GraphedStep(graph, st_img, st_in, st_tg, loss)
 
     @torch.no_grad()
     def eval_loss(self, images, decoder_input_tokens, target_tokens) -> torch.Tensor:

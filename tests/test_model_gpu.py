@@ -210,3 +210,29 @@ def test_dropout_train_step_matches_oracle_with_same_masks():
               "decoder.transformer_decoder.layers.0.self_attn.in_proj_weight", "decoder.token_embedding.weight",
               "decoder.transformer_decoder.layers.1.multihead_attn.in_proj_weight"]:
         torch.testing.assert_close(grads[k].cpu(), leaves[k].grad, rtol=2e-3, atol=2e-5)
+
+
+def test_graphed_step_matches_eager():
+    """make_graphed_step (one hipGraph per step) reproduces eager steps (dropout on, bf16)."""
+    import optim
+    meta, T = FX.load("tiny_vit_patches")
+    res = []
+    for graphed in (False, True):
+        m, _ = build_model(meta, torch.bfloat16, dropout=0.1)
+        m.train()
+        opt = optim.AdamW(m.store, lr=1e-3)
+        imgs, di, tg = FX.inputs(meta, 0)
+        imgs, di, tg = imgs.cuda(), di.cuda(), tg.cuda()
+        losses = []
+        if graphed:
+            g = m.make_graphed_step(opt, imgs, di, tg, 5.0)
+            for _ in range(3):
+                losses.append(g().item())
+        else:
+            for _ in range(3):
+                losses.append(m.train_step(imgs, di, tg).item())
+                opt.step(5.0)
+        res.append((losses, m.store.master.clone()))
+    (l0, p0), (l1, p1) = res
+    assert all(abs(a - b) < 1e-3 for a, b in zip(l0, l1)), (l0, l1)
+    torch.testing.assert_close(p1, p0, rtol=0, atol=1e-4)
