@@ -32,37 +32,131 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
+PMC_SUMMARY = "r01_bench_pmc.json"
 METRIC = "image-caption pairs/sec (train step), 6L/d512 decoder + ViT-B/16, 1/2/4/8 GPU"
 
 
+class HipEvent:
+    """hipEvent created with hipEventDisableSystemFence: a timing-only event whose record does not
+    write back / invalidate caches (a default event's system-scope fence adds ~8 us to every
+    bracketed launch). Recorded on the stream the kernels are launched on (native.stream_ptr())."""
+    _hip = None
+    DISABLE_SYSTEM_FENCE = 0x20000000
+
+    def __init__(self):
+        import ctypes
+        if HipEvent._hip is None:
+            h = ctypes.CDLL("libamdhip64.so.7")  # soname: resolves to the runtime torch already loaded
+            h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            HipEvent._hip = h
+        self.ev = ctypes.c_void_p()
+        if HipEvent._hip.hipEventCreateWithFlags(ctypes.byref(self.ev), self.DISABLE_SYSTEM_FENCE) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+
+    def record(self, stream):
+        if HipEvent._hip.hipEventRecord(self.ev, stream) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def seconds_to(self, other):
+        import ctypes
+        ms = ctypes.c_float()
+        if HipEvent._hip.hipEventElapsedTime(ctypes.byref(ms), self.ev, other.ev) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value * 1e-3
+
+    def __del__(self):
+        if HipEvent._hip is not None and self.ev:
+            HipEvent._hip.hipEventDestroy(self.ev)
+
+
 class GemmProbe:
-    """HIP events around every GEMM launch, grouped by kernel instance (a_layout, b_layout)."""
+    """Times the GEMM kernels of the eager step two ways, with fence-free HIP events on the launch
+    stream: (1) an event pair around every launch in place; (2) the launches of one step replayed
+    in their original order, back-to-back, `passes` times, between ONE event pair per kernel
+    instance (a_layout, b_layout) -- this is the per-launch kernel duration (event markers between
+    kernels add a dispatch ramp that the kernel itself does not spend; rocprofv3's per-dispatch
+    average, profiles/r01_bench_kernel_stats.csv, is the cross-check)."""
 
     def __init__(self):
         self.rec = []
         self.cur = None
+        self.step = []
 
-    def before(self, dt, al, bl, M, N, K):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        self.cur = (e0, (al, bl), 2.0 * M * N * K)
+    def new_step(self):
+        self.step = []
 
-    def after(self):
-        e1 = torch.cuda.Event(enable_timing=True)
-        e1.record()
-        e0, key, fl = self.cur
-        self.rec.append((e0, e1, key, fl))
+    def before(self, dt, al, bl, M, N, K, nbytes):
+        import native
+        e0 = HipEvent()
+        e0.record(native.stream_ptr())
+        self.cur = (e0, (al, bl), 2.0 * M * N * K, nbytes)
+
+    def after(self, g):
+        import ctypes
+        import native
+        e1 = HipEvent()
+        s = native.stream_ptr()
+        e1.record(s)
+        e0, key, fl, nb = self.cur
+        self.rec.append((e0, e1, key, fl, nb))
+        gc = type(g)()
+        ctypes.memmove(ctypes.byref(gc), ctypes.byref(g), ctypes.sizeof(g))
+        self.step.append((key, gc, s, fl, nb))
 
     def summary(self):
+        """{(a_layout, b_layout): [seconds, flops, launches, algorithmic bytes]} from the in-place pairs."""
         torch.cuda.synchronize()
         agg = {}
-        for e0, e1, key, fl in self.rec:
-            t = e0.elapsed_time(e1) * 1e-3
-            a = agg.setdefault(key, [0.0, 0.0, 0])
+        for e0, e1, key, fl, nb in self.rec:
+            t = e0.seconds_to(e1)
+            a = agg.setdefault(key, [0.0, 0.0, 0, 0])
             a[0] += t
             a[1] += fl
             a[2] += 1
+            a[3] += nb
         return agg
+
+    def replay(self, passes=3):
+        """{(a_layout, b_layout): [seconds, flops, launches, algorithmic bytes]} over the replays of the
+        last recorded step (modifies activations/grads in place: run after everything measured)."""
+        import native
+        torch.cuda.synchronize()
+        out = {}
+        for key in sorted({k for k, *_ in self.step}):
+            launches = [r for r in self.step if r[0] == key]
+            s = launches[0][2]
+            for _, g, _, _, _ in launches:  # warm the code object / caches once
+                native.gemm_relaunch(g, s)
+            e0, e1 = HipEvent(), HipEvent()
+            e0.record(s)
+            for _ in range(passes):
+                for _, g, _, _, _ in launches:
+                    native.gemm_relaunch(g, s)
+            e1.record(s)
+            torch.cuda.synchronize()
+            n = passes * len(launches)
+            out[key] = [e0.seconds_to(e1), passes * sum(r[3] for r in launches), n,
+                        passes * sum(r[4] for r in launches)]
+        return out
+
+
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary (FETCH_SIZE and
+    WRITE_SIZE passes of tools/profile_r01.sh over this same command, condensed by
+    tools/rocpd_summary.py); None when no summary is present."""
+    path = os.path.join(ROOT, "profiles", PMC_SUMMARY)
+    try:
+        with open(path) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    for name, e in ks.items():
+        if name.startswith(kernel_prefix) and "hbm_bytes_per_launch" in e:
+            return e["hbm_bytes_per_launch"], f"profiles/{PMC_SUMMARY}"
+    return None, None
 
 
 def build(args, rank):
@@ -201,20 +295,32 @@ def main():
         probe = GemmProbe()
         native.set_gemm_probe(probe)
         for _ in range(min(args.steps, 5)):  # eager replay of the same step (events need eager launches)
+            # park the GPU on a ~50 ms spin so the host enqueues the whole step ahead of it: the event
+            # pairs then time back-to-back kernels, not the host's launch latency
+            torch.cuda.synchronize()
+            torch.cuda._sleep(120_000_000)
+            probe.new_step()
             eager_step()
             opt.step(5.0)
         native.set_gemm_probe(None)
-        agg = probe.summary()
+        inplace = probe.summary()
+        agg = probe.replay()
         names = {(0, 0): "gemm_bf16_kernel<0,0> (NT: forward)", (0, 1): "gemm_bf16_kernel<0,1> (NN: dX)",
                  (1, 1): "gemm_bf16_kernel<1,1> (TN: dW)", (1, 0): "gemm_bf16_kernel<1,0>"}
         key = max(agg, key=lambda k: agg[k][0])
-        t, fl, n = agg[key]
+        t, fl, n, nb = agg[key]
         ach = fl / t / 1e12
+        traffic, src = pmc_traffic(f"gemm_bf16_kernel<{key[0]}, {key[1]},")
         out["roofline"] = {"bound": "mfma", "kernel": names.get(key, str(key)), "achieved": round(ach, 1),
                            "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
-                           "traffic": None, "launches": n, "avg_launch_us": round(1e6 * t / n, 2)}
+                           "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
+                           "algorithmic_bytes_per_launch": round(nb / n), "flop_per_launch": round(fl / n),
+                           "launches": n, "avg_launch_us": round(1e6 * t / n, 2),
+                           "avg_launch_us_event_bracketed": round(1e6 * inplace[key][0] / inplace[key][2], 2),
+                           "timing": "one step's launches of this kernel replayed in order, back-to-back, 3 passes, "
+                                     "between fence-free HIP events on the launch stream"}
         out["gemm_breakdown"] = {names.get(k, str(k)): {"tflops": round(v[1] / v[0] / 1e12, 1),
-                                                        "ms_per_step": round(1e3 * v[0] / min(args.steps, 5), 3)}
+                                                        "ms_per_step": round(1e3 * v[0] * inplace[k][2] / v[2] / min(args.steps, 5), 3)}
                                  for k, v in agg.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(model, args)

@@ -162,17 +162,26 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
                  0 if workspace is None else workspace.numel() * workspace.element_size())
     probe = _gemm_probe
     if probe is not None:
-        probe.before(dt, a_layout, b_layout, M, N, K)
+        # algorithmic bytes: operands once, output once (+ read-back of C / residual / aux when used)
+        esz = A.element_size()
+        nbytes = (M * K + N * K) * esz + M * N * C.element_size() * (2 if accumulate else 1)
+        nbytes += M * N * esz * ((residual is not None) + (aux is not None))
+        probe.before(dt, a_layout, b_layout, M, N, K, nbytes)
     _check(lib().mit_gemm(ctypes.byref(g), stream_ptr()), "mit_gemm")
     if probe is not None:
-        probe.after()
+        probe.after(g)
 
 
 _gemm_probe = None
 
 
+def gemm_relaunch(g, stream) -> None:
+    """Launch a recorded mit_gemm_args again (bench.py replays one step's GEMMs back-to-back)."""
+    _check(lib().mit_gemm(ctypes.byref(g), stream), "mit_gemm")
+
+
 def set_gemm_probe(probe):
-    """Install an object with before(dtype, a_layout, b_layout, M, N, K) / after() called around
+    """Install an object with before(dtype, a_layout, b_layout, M, N, K, nbytes) / after(args) called around
     every GEMM launch (bench.py records HIP events there to time the GEMM kernels in place)."""
     global _gemm_probe
     _gemm_probe = probe

@@ -1,0 +1,72 @@
+"""Condense rocprofv3 rocpd databases (tools/profile_r01.sh) into the summaries committed under
+profiles/ (the --stats tables themselves, run_kernel_stats.csv, are copied there as they are):
+
+  <prefix>_pmc.json          per-kernel FETCH_SIZE / WRITE_SIZE averages (separate passes) and the
+                             HBM bytes per launch with the gfx950 correction of
+                             MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of 16-B/lane
+                             streaming reads -> x2; WRITE_SIZE exact for 16-B stores; both in KiB)
+
+    python tools/rocpd_summary.py --trace D/trace/run_results.db --fetch D/fetch/run_results.db \
+        --write D/write/run_results.db --out profiles/r01
+"""
+import argparse
+import json
+import re
+import sqlite3
+
+
+def short(name: str) -> str:
+    """Demangled kernel names carry long parameter lists; keep the template head."""
+    n = re.sub(r"^void ", "", name)
+    n = n.replace("(anonymous namespace)::", "")
+    m = re.match(r"^_ZN12_GLOBAL__N_1\d+(\w+?)I", n)
+    if m:
+        return m.group(1)
+    return n.split("(")[0] if not n.startswith("(") else n
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, total_calls, total_duration, average, percentage from top_kernels").fetchall()
+    return [(short(r[0]), r[0], int(r[1]), float(r[2]), float(r[3]), float(r[4])) for r in rows]
+
+
+def pmc(db, counter):
+    c = sqlite3.connect(db)
+    rows = c.execute("select kernel_name, count(*), avg(value), avg(duration) from counters_collection "
+                     "where counter_name = ? group by kernel_name", (counter,)).fetchall()
+    return {short(r[0]): {"launches": int(r[1]), "avg_kib": float(r[2]), "avg_ns": float(r[3])} for r in rows}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--command", default="")
+    a = ap.parse_args()
+    ks = kernel_stats(a.trace)
+    fe, wr = pmc(a.fetch, "FETCH_SIZE"), pmc(a.write, "WRITE_SIZE")
+    out = {"command": a.command,
+           "correction": "hbm_bytes = 2 * FETCH_SIZE + WRITE_SIZE, both KiB (gfx950: FETCH_SIZE counts half of "
+                         "16-B/lane streaming reads; MI355X_MICROARCH.md HBM section)",
+           "kernels": {}}
+    trace_avg = {s: avg for s, _, n, tot, avg, pct in ks}
+    for k in sorted(set(fe) | set(wr), key=lambda k: -(fe.get(k, {}).get("avg_kib", 0) * fe.get(k, {}).get("launches", 0))):
+        f_, w_ = fe.get(k), wr.get(k)
+        e = {"launches": (f_ or w_)["launches"], "avg_us_pmc_pass": round((f_ or w_)["avg_ns"] / 1e3, 3),
+             "fetch_kib_per_launch": None if f_ is None else round(f_["avg_kib"], 1),
+             "write_kib_per_launch": None if w_ is None else round(w_["avg_kib"], 1),
+             "avg_us_trace": None if k not in trace_avg else round(trace_avg[k], 3)}
+        if f_ is not None and w_ is not None:
+            e["hbm_bytes_per_launch"] = round((2 * f_["avg_kib"] + w_["avg_kib"]) * 1024)
+        out["kernels"][k] = e
+    with open(a.out + "_pmc.json", "w") as f:
+        json.dump(out, f, indent=1)
+    for s, _, n, tot, avg, pct in ks[:12]:
+        print(f"{s:60s} {n:6d} {avg:9.2f} us {pct:6.2f}%")
+
+
+if __name__ == "__main__":
+    main()
