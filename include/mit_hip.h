@@ -84,6 +84,10 @@ typedef struct {
 } mit_gemm_args;
 int mit_gemm(const mit_gemm_args* args, void* stream);
 long mit_gemm_workspace_bytes(long M, long N, long K);
+/* Tile-kernel choice for bf16 GEMMs: 0 = per shape (default; env MIT_GEMM_VARIANT seeds it),
+ * 1 = 128x128 kernel only, 2 = 256x256 kernel wherever split-K is not planned. Results are
+ * identical up to fp32 summation order; a tuning / test knob, not a numerics switch. */
+int mit_gemm_set_variant(int variant);
 
 /* ---------------------------------------------------------------------------------------------
  * LayerNorm over the last dim, fp32 statistics.

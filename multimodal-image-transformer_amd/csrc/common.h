@@ -87,6 +87,20 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+// GELU (erf form) without ocml's branchy erff, for bf16 epilogues: Phi(x) = 1 - 0.5*erfc(x/sqrt2)
+// with erfc(a) = t*P(t)*exp(-a^2), t = 1/(1 + 0.3275911 a) (Abramowitz-Stegun 7.1.26, |error| of
+// erf <= 1.5e-7), evaluated on |x| so the negative tail keeps its relative accuracy (no 1 - 1).
+// ~12 VALU ops incl. one v_rcp and one v_exp; fp32 parity mode keeps gelu_erf.
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float a = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float h = 0.5f * p * t * __expf(-a * a);  // 0.5 * erfc(|x|/sqrt2) = Phi(-|x|)
+  return x * (x >= 0.0f ? 1.0f - h : h);
+}
 
 // error plumbing shared by every C-ABI entry point (capi.cpp)
 int mit_set_error(const char* fmt, ...);

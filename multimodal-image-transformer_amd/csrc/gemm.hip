@@ -7,20 +7,26 @@
 //   B: MIT_K_CONTIG  -> B[n*ldb + k]      (nn.Linear weight W[out,in] in Y = X W^T)
 //      MIT_MN_CONTIG -> B[k*ldb + n]      (W in dX = dY W, X in dW = dY^T X)
 //
-// bf16 path: 128x128x64 block tile, 4 waves (2x2), each wave 64x64 = 4x4 tiles of
-// v_mfma_f32_16x16x32_bf16, fp32 accumulation.
-//   * staging: buffer loads (SRSRC descriptors) into registers -> LDS double buffer, one barrier
-//     per K step. Edge tiles need no branches: an out-of-range chunk gets an offset past the
-//     descriptor's num_records and the hardware returns zeros.
+// Two bf16 tile kernels, fp32 accumulation on v_mfma_f32_16x16x32_bf16, both staging operands
+// HBM -> LDS by LDS-DMA (buffer_load ... lds) with the swizzle applied on the source address:
+//   * gemm_bf16_kernel: 128x128x64, 4 waves (2x2, 64x64 each), 2 blocks per CU, 2 LDS stages,
+//     optional split-K with fused bias-gradient row sums (weight gradients).
+//   * gemm256_kernel: 256x256x64, 8 waves (2x4, 128x64 each), 1 block per CU, 8-phase ping-pong
+//     schedule with half-tile DMA granularity and counted vmcnt (large GEMMs: the encoder's
+//     M = B*197 rows). mit_gemm picks per shape with an occupancy-quantised cost model.
 //   * K-contig tiles are XOR-swizzled for conflict-free ds_read_b128 fragment reads; MN-contig
 //     tiles are read with ds_read_b64_tr_b16 (CDNA4 hardware transpose) so one kernel serves
-//     NT / NN / TN without materialising a transpose.
-//   * epilogue: the fp32 accumulator tile is staged through LDS, then every thread applies
-//     bias / activation / relu-dropout mask / dropout / residual to 8 consecutive columns and
-//     writes 16 bytes (coalesced rows instead of the MFMA layout's 4-row x 16-column scatter).
-//   * tile order: XCD-aware remap + 8-row grouping so tiles sharing A/B panels share an L2.
+//     NT / NN / TN without materialising a transpose. Out-of-range chunks get a buffer offset
+//     past num_records and read as zeros: no edge branches in the main loops.
+//   * epilogue: accumulators staged through LDS, then each lane applies the fused epilogue to 8
+//     consecutive columns and writes 16 bytes. The activation and dropout are TEMPLATE
+//     parameters (an 8-wide GELU / dropout-hash epilogue evaluated behind runtime flags costs
+//     ~20 % of a K=768 GEMM); bias / residual / aux-mask / f32-accumulate stay runtime flags.
+//   * tile order: XCD-aware remap + row grouping so tiles sharing A/B panels share an L2.
 // fp32 path (parity mode): a plain LDS-tiled FMA kernel with the identical epilogue semantics.
 #include <stdlib.h>
+
+#include <cmath>
 
 #include "common.h"
 
@@ -45,17 +51,23 @@ struct Epi {
   int vec;  // 16-B vector epilogue legal (alignments / leading dims / N multiple of 8)
 };
 
-__device__ __forceinline__ float epi_pre(const Epi& e, float v, float bias) {
-  v = v * e.alpha + bias;
-  if (e.act == MIT_ACT_RELU) v = fmaxf(v, 0.0f);
-  else if (e.act == MIT_ACT_GELU) v = gelu_erf(v);
-  else if (e.act == MIT_ACT_QUICK_GELU) v = quick_gelu(v);
+constexpr int ACT_RT = -1;  // activation read from Epi::act at run time (generic instance)
+
+// FAST: bf16 vector epilogues use the branch-free GELU (gelu_fast, |err| ~1e-7, far below bf16
+// rounding); the scalar / fp32-parity path keeps ocml's erff
+template <int ACT, bool FAST = false>
+__device__ __forceinline__ float act_apply(int rt, float v) {
+  const int a = ACT == ACT_RT ? rt : ACT;
+  if (a == MIT_ACT_RELU) v = fmaxf(v, 0.0f);
+  else if (a == MIT_ACT_GELU) v = FAST ? gelu_fast(v) : gelu_erf(v);
+  else if (a == MIT_ACT_QUICK_GELU) v = quick_gelu(v);
   return v;
 }
 
+// scalar epilogue (ragged column edges and the fp32 kernel): every feature at run time
 template <typename T>
 __device__ __forceinline__ void epi_store(const Epi& e, void* C, long ldc, long N, long r, long c, float v) {
-  v = epi_pre(e, v, e.bias ? e.bias[c] : 0.0f);
+  v = act_apply<ACT_RT>(e.act, v * e.alpha + (e.bias ? e.bias[c] : 0.0f));
   if (e.aux) v *= (to_f(((const T*)e.aux)[r * e.ld_aux + c]) > 0.0f) ? e.aux_scale : 0.0f;
   if (e.dropout) v *= drop_mul(site_key(e.seed, e.site), (uint64_t)r * (uint64_t)N + (uint64_t)c, e.thresh, e.dscale);
   if (e.res) v += to_f(((const T*)e.res)[r * e.ldr + c]);
@@ -68,8 +80,9 @@ __device__ __forceinline__ void epi_store(const Epi& e, void* C, long ldc, long 
   }
 }
 
-// 8 consecutive columns [c, c+8) of row r; vector loads / stores (bf16 operands)
-__device__ __forceinline__ void epi_store8_bf16(const Epi& e, void* C, long ldc, long N, long r, long c, float* v) {
+// 8 consecutive columns [c, c+8) of row r (bf16 operands), vector loads / stores
+template <int ACT, bool DROP>
+__device__ __forceinline__ void epi8(const Epi& e, void* C, long ldc, long N, long r, long c, float* v) {
   float b[8];
   if (e.bias) {
     const f32x4 b0 = *(const f32x4*)(e.bias + c), b1 = *(const f32x4*)(e.bias + c + 4);
@@ -79,13 +92,17 @@ __device__ __forceinline__ void epi_store8_bf16(const Epi& e, void* C, long ldc,
     for (int k = 0; k < 8; ++k) b[k] = 0.f;
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) v[k] = epi_pre(e, v[k], b[k]);
+  for (int k = 0; k < 8; ++k) v[k] = v[k] * e.alpha + b[k];
+  if (ACT != MIT_ACT_NONE) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = act_apply<ACT, true>(e.act, v[k]);
+  }
   if (e.aux) {
     const bf16x8 a = *(const bf16x8*)((const bf16*)e.aux + r * e.ld_aux + c);
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= ((float)a[k] > 0.0f) ? e.aux_scale : 0.0f;
   }
-  if (e.dropout) {
+  if (DROP && e.dropout) {
     const uint64_t key = site_key(e.seed, e.site);
     const uint64_t base = (uint64_t)r * (uint64_t)N + (uint64_t)c;
 #pragma unroll
@@ -113,8 +130,19 @@ __device__ __forceinline__ void epi_store8_bf16(const Epi& e, void* C, long ldc,
   }
 }
 
+// one staged row segment: vector epilogue when legal, else the scalar one per in-range column
+template <int ACT, bool DROP>
+__device__ __forceinline__ void epi_row8(const Epi& e, void* C, long ldc, long N, long gr, long gc, float* v) {
+  if (e.vec && gc + 8 <= N) {
+    epi8<ACT, DROP>(e, C, ldc, N, gr, gc, v);
+  } else {
+    for (int k = 0; k < 8; ++k)
+      if (gc + k < N) epi_store<bf16>(e, C, ldc, N, gr, gc + k, v[k]);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
-// bf16 MFMA kernel
+// operand tiles in LDS
 // ------------------------------------------------------------------------------------------------
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE_BYTES = BM * BK * 2;          // 16 KiB per operand per stage
@@ -129,52 +157,17 @@ __device__ __forceinline__ int koff(int r, int c) { return r * 128 + ((c ^ ((r >
 __device__ __forceinline__ int mn_swz(int kr) { return ((kr & 3) | ((((kr >> 2) ^ (kr >> 3)) & 1) << 2)) << 5; }
 __device__ __forceinline__ int mnoff(int kr, int byte_in_row) { return kr * 256 + (byte_in_row ^ mn_swz(kr)); }
 
-template <int LAY>
-struct Stage {
-  u32x4 r[4];
-  // BM (or BN) x BK tile at (row0 = m/n offset, k0) -> registers; out-of-range chunks read 0
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, long ld, long rows_total, long K, long row0, long k0,
-                                       int tid) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + 256 * i;
-      bool ok;
-      long off;
-      if (LAY == MIT_K_CONTIG) {
-        const int rr = id >> 3, c = id & 7;
-        ok = (row0 + rr < rows_total) && (k0 + c * 8 < K);
-        off = (row0 + rr) * ld + k0 + c * 8;
-      } else {
-        const int kr = id >> 4, c = id & 15;
-        ok = (k0 + kr < K) && (row0 + c * 8 < rows_total);
-        off = (k0 + kr) * ld + row0 + c * 8;
-      }
-      const uint32_t boff = ok ? (uint32_t)(off * 2) : OOB;
-      r[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)boff, 0, 0));
-    }
-  }
-  __device__ __forceinline__ void store(char* lds, int tid) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + 256 * i;
-      int off;
-      if (LAY == MIT_K_CONTIG) off = koff(id >> 3, id & 7);
-      else off = mnoff(id >> 4, (id & 15) * 16);
-      *(u32x4*)(lds + off) = r[i];
-    }
-  }
-};
-
 // LDS-DMA fill of one 16 KiB operand tile: 1024 16-B chunks = 16 wave-instructions, wave w issues
-// w*4 .. w*4+3. The DMA writes each instruction's 1 KiB linearly (base + lane*16), so the swizzle is
-// applied to the SOURCE address instead: linear position p holds logical chunk phys ^ swizzle(row)
-// (the XOR is an involution), which reproduces exactly the koff / mnoff images read by frag().
-template <int LAY>
+// w*NPW .. w*NPW+NPW-1 (NPW = 16 / waves). The DMA writes each instruction's 1 KiB linearly
+// (base + lane*16), so the swizzle is applied to the SOURCE address instead: linear position p holds
+// logical chunk phys ^ swizzle(row) (the XOR is an involution), which reproduces exactly the
+// koff / mnoff images read by frag().
+template <int LAY, int NPW = 4>
 __device__ __forceinline__ void glds_tile(__amdgpu_buffer_rsrc_t rs, char* tile, long ld, long rows_total, long K,
                                           long row0, long k0, int w, int lane) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int inst = w * 4 + j;
+  for (int j = 0; j < NPW; ++j) {
+    const int inst = w * NPW + j;
     const int id = inst * 64 + lane;
     bool ok;
     long off;
@@ -211,7 +204,28 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int rbase, int kk, int l
   }
 }
 
-template <int ALAY, int BLAY, bool GLDS>
+// XCD-aware block order: hardware block ids round-robin over the 8 XCDs; give each XCD a
+// contiguous run of tiles (bijective for any grid size) so neighbours share its L2 (guide §5.5 T1)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, rr = nwg % 8, x = bid % 8, y = bid / 8;
+  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + y;
+}
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+// sum of the 8 bf16 of a fragment into r (fused bias-gradient row sums), v_dot2_f32_bf16
+__device__ __forceinline__ float frag_rowsum(bf16x8 a, float r) {
+  const bf16x2 one2 = {(bf16)1.0f, (bf16)1.0f};
+  r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 0, 1), one2, r, false);
+  r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 2, 3), one2, r, false);
+  r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 4, 5), one2, r, false);
+  r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 6, 7), one2, r, false);
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// bf16 MFMA kernel, 128x128 block tile
+// ------------------------------------------------------------------------------------------------
+template <int ALAY, int BLAY, int ACT, bool DROP>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                         long M, long N, long K, long lda, long ldb, long ldc,
                                                         int a_bytes, int b_bytes, Epi e, int ksplit, long kchunk,
@@ -220,15 +234,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
-  // XCD-aware tile order: hardware block ids round-robin over the 8 XCDs; give each XCD a
-  // contiguous run of tiles (bijective for any grid size) so neighbours share its L2 (guide §5.5 T1).
   const int nbn = (int)((N + BN - 1) / BN), nbm = (int)((M + BM - 1) / BM);
   const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
-  int bid = blockIdx.x;
-  {
-    const int q = nwg / 8, rr = nwg % 8, x = bid % 8, y = bid / 8;
-    bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + y;
-  }
+  int bid = xcd_remap(blockIdx.x, nwg);
   // split-K: slice `split` covers k in [kb, ke)
   const int split = bid / ntiles;
   bid -= split * ntiles;
@@ -254,15 +262,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fused row sums of A (bias gradients): one extra MFMA against a ones fragment, only in the
-  // blocks of the first column tile and the waves of its first column half (wave-uniform branch)
-  // (compiled only into the TN instance — the weight-gradient GEMMs — so the other instances
-  // keep their register budget)
+  // fused row sums of A (bias gradients): only the TN instance (weight-gradient GEMMs), blocks of
+  // the first column tile, waves of its first column half (wave-uniform branch)
   const bool do_rs = ALAY == MIT_MN_CONTIG && BLAY == MIT_MN_CONTIG && rowsum != nullptr && bn == 0 && wn == 0;
-  // per lane: partial row sums of its 8 k-values of rows rbase + (lane&15), via v_dot2_f32_bf16
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
-  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-  const bf16x2 one2 = {(bf16)1.0f, (bf16)1.0f};
 
   const int nk = (int)((ke - kb + BK - 1) / BK);
   auto compute = [&](int cur) {
@@ -279,57 +282,27 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       if (do_rs) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          rs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(af[i], af[i], 0, 1), one2, rs[i], false);
-          rs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(af[i], af[i], 2, 3), one2, rs[i], false);
-          rs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(af[i], af[i], 4, 5), one2, rs[i], false);
-          rs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(af[i], af[i], 6, 7), one2, rs[i], false);
-        }
+        for (int i = 0; i < 4; ++i) rs[i] = frag_rowsum(af[i], rs[i]);
       }
     }
   };
 
-  if constexpr (GLDS) {
-    // direct-to-LDS buffer loads (LDS-DMA): no staging registers, no ds_write pass. Two stages:
-    // the next tile's DMA is in flight while this tile computes; counted vmcnt + raw barriers
-    // (a __syncthreads() would drain the in-flight DMA with vmcnt(0), guide §5).
-    glds_tile<ALAY>(ra, AS(0), lda, M, ke, m0, kb, wid, lane);
-    glds_tile<BLAY>(rb, BS(0), ldb, N, ke, n0, kb, wid, lane);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) {
-        glds_tile<ALAY>(ra, AS(cur ^ 1), lda, M, ke, m0, kb + (long)(kt + 1) * BK, wid, lane);
-        glds_tile<BLAY>(rb, BS(cur ^ 1), ldb, N, ke, n0, kb + (long)(kt + 1) * BK, wid, lane);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this tile's 8 DMAs done, next 8 in flight
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
-      compute(cur);
-      __builtin_amdgcn_s_barrier();  // every wave is done reading buffer cur before it is refilled
+  // LDS-DMA, two stages: the next tile's DMA is in flight while this tile computes; counted vmcnt
+  // + raw barriers (a __syncthreads() would drain the in-flight DMA with vmcnt(0), guide §5)
+  glds_tile<ALAY>(ra, AS(0), lda, M, ke, m0, kb, wid, lane);
+  glds_tile<BLAY>(rb, BS(0), ldb, N, ke, n0, kb, wid, lane);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      glds_tile<ALAY>(ra, AS(cur ^ 1), lda, M, ke, m0, kb + (long)(kt + 1) * BK, wid, lane);
+      glds_tile<BLAY>(rb, BS(cur ^ 1), ldb, N, ke, n0, kb + (long)(kt + 1) * BK, wid, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this tile's 8 DMAs done, next 8 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-  } else {
-    Stage<ALAY> sa;
-    Stage<BLAY> sb;
-    sa.load(ra, lda, M, ke, m0, kb, tid);
-    sb.load(rb, ldb, N, ke, n0, kb, tid);
-    sa.store(AS(0), tid);
-    sb.store(BS(0), tid);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      const bool more = kt + 1 < nk;
-      if (more) {
-        sa.load(ra, lda, M, ke, m0, kb + (long)(kt + 1) * BK, tid);
-        sb.load(rb, ldb, N, ke, n0, kb + (long)(kt + 1) * BK, tid);
-      }
-      compute(cur);
-      if (more) {
-        sa.store(AS(cur ^ 1), tid);
-        sb.store(BS(cur ^ 1), tid);
-      }
-      __syncthreads();
-    }
+    __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
+    compute(cur);
+    __builtin_amdgcn_s_barrier();  // every wave is done reading buffer cur before it is refilled
   }
 #undef AS
 #undef BS
@@ -362,7 +335,6 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     const int r = id >> 4, c8 = (id & 15) * 8;
     const long gr = m0 + r, gc = n0 + c8;
     if (gr >= M || gc >= N) continue;
-    float v[8];
     const f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
     if (ksplit > 1) {  // raw fp32 partial slab; gemm_splitk_reduce applies the (plain) epilogue
       f32x4* o = (f32x4*)(ws + ((long)split * M + gr) * N + gc);
@@ -370,13 +342,291 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
       o[1] = hi;
       continue;
     }
-    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3]; v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-    if (e.vec && gc + 8 <= N) {
-      epi_store8_bf16(e, C, ldc, N, gr, gc, v);
-    } else {
-      for (int k = 0; k < 8; ++k)
-        if (gc + k < N) epi_store<bf16>(e, C, ldc, N, gr, gc + k, v[k]);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    epi_row8<ACT, DROP>(e, C, ldc, N, gr, gc, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// bf16 MFMA kernel, 256x256 block tile (large GEMMs: the encoder's M = B*197 rows)
+//
+// 8 waves as 2 (M) x 4 (N); each wave owns a 128x64 output tile = 8x4 accumulators. LDS: two
+// K-tile buffers (BK = 64), each cut into four 16 KiB "half-tiles" (A rows 0-127 / 128-255,
+// B rows 0-127 / 128-255) whose images are exactly the 128-row tiles of the kernel above (same
+// swizzles, same frag() reads, all four layouts); the epilogue reuses the space.
+//
+// Each K-tile is consumed in 4 phases (one 64x32 quadrant of the wave's tile x K=64 = 16 MFMAs):
+//   q0: read A rows 0-63 + B cols 0-31    q1: read B cols 32-63
+//   q2: read A rows 64-127                q3: no reads (A hi x B lo from registers)
+// A phase = {fragment ds_reads, one half-tile LDS-DMA issue, [counted vmcnt]} barrier
+//           {16 MFMAs} barrier.
+// Wave group wr = 1 runs one barrier behind wr = 0 (ping-pong): on every SIMD one wave issues
+// MFMAs while its partner reads fragments / issues DMA.
+// Buffer hazards (phase numbers within the 2-K-tile iteration, tile t in buf0, t+1 in buf1):
+//   DMA schedule   ph0 B1(t+1) ph1 A0(t+1) ph2 A1(t+1) ph3 B0(t+2) ph4 B1(t+2) ph5 A0(t+2) ph6 A1(t+2)
+//                  ph7 B0(t+3)
+//   WAR: a half is refilled >= 2 phases after its last ds_read (buf0 B read ph0-1 -> refilled ph3-4,
+//        A read ph0,ph2 -> ph5-6; buf1 B ph4-5 -> ph7,ph0'; A ph4,ph6 -> ph1',ph2'), which with the
+//        one-barrier stagger still orders the partner group's reads before the DMA.
+//   RAW: ph3 waits vmcnt(2) (every half of t+1 landed, ph3's own DMA in flight) and ph7 vmcnt(2)
+//        (t+2); vmcnt(0) where that younger DMA was not issued. The first read is one phase later,
+//        behind both groups' barriers.
+// ------------------------------------------------------------------------------------------------
+constexpr int B2 = 256;
+constexpr int HALF_BYTES = 128 * 64 * 2;  // one 128-row x BK half-tile
+constexpr int BUF_BYTES = 4 * HALF_BYTES;
+constexpr int EPI_LD = 68;                // per-wave fp32 epilogue stage [64][68]
+constexpr int SMEM2_BYTES = (2 * BUF_BYTES > 8 * 64 * EPI_LD * 4) ? 2 * BUF_BYTES : 8 * 64 * EPI_LD * 4;
+
+// Per-lane LDS-DMA source plan for one operand (8 waves x 2 wave-instructions per half-tile):
+// byte offsets of this lane's two 16-B chunks in each half at K-tile 0 (OOB when the row / column
+// is out of range), the chunk's k inside the tile, and the per-K-tile byte step. Precomputed once
+// so the main loop issues each DMA with one compare and one add.
+template <int LAY>
+struct DmaPlan {
+  uint32_t base[2][2];
+  int kc[2];
+  uint32_t step;
+  __device__ __forceinline__ void init(long ld, long rows_total, long row0, long kb, int w, int lane) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int id = (w * 2 + j) * 64 + lane;
+      if (LAY == MIT_K_CONTIG) {
+        const int r = id >> 3, c = (id & 7) ^ ((r >> 1) & 7);
+        kc[j] = c * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const long row = row0 + h * 128 + r;
+          base[h][j] = row < rows_total ? (uint32_t)((row * ld + kb + c * 8) * 2) : OOB;
+        }
+      } else {
+        const int kr = id >> 4, c = (id & 15) ^ (mn_swz(kr) >> 4);
+        kc[j] = kr;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const long col = row0 + h * 128 + c * 8;
+          base[h][j] = col < rows_total ? (uint32_t)(((kb + kr) * ld + col) * 2) : OOB;
+        }
+      }
     }
+    step = LAY == MIT_K_CONTIG ? (uint32_t)(BK * 2) : (uint32_t)(BK * ld * 2);
+  }
+  // dst = this wave's 2 KiB slice of the half-tile; t = K-tile index
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* dst, int h, int t, int klen) const {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t boff = (t * BK + kc[j] < klen) ? base[h][j] + (uint32_t)t * step : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
+                                               boff, 0, 0, 0);
+    }
+  }
+};
+
+// workgroup barrier that is also a compiler scheduling / memory fence but emits no vmcnt wait
+// (an in-flight LDS-DMA must survive it)
+__device__ __forceinline__ void bar_raw() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int ALAY, int BLAY, int ACT, bool DROP>
+__global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
+                                                      long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
+                                                      int b_bytes, Epi e, int ksplit, long kchunk,
+                                                      float* __restrict__ ws, float* __restrict__ rowsum) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  const int nbn = (int)((N + B2 - 1) / B2), nbm = (int)((M + B2 - 1) / B2);
+  const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
+  int bid = xcd_remap(blockIdx.x, nwg);
+  const int split = bid / ntiles;
+  bid -= split * ntiles;
+  const long kb = (long)split * kchunk, ke = min(K, kb + kchunk);
+  const int GROUP = 4;
+  const int group_id = bid / (GROUP * nbn);
+  const int first_m = group_id * GROUP;
+  const int gsize = min(nbm - first_m, GROUP);
+  const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
+  const int bn = (bid % (GROUP * nbn)) / gsize;
+  const long m0 = (long)bm * B2, n0 = (long)bn * B2;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr bool TN = ALAY == MIT_MN_CONTIG && BLAY == MIT_MN_CONTIG;
+  const bool do_rs = TN && rowsum != nullptr && bn == 0 && wc == 0;
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)((ke - kb + BK - 1) / BK);
+  DmaPlan<ALAY> pa;
+  DmaPlan<BLAY> pb;
+  pa.init(lda, M, m0, kb, wid, lane);
+  pb.init(ldb, N, n0, kb, wid, lane);
+  const int klen = (int)(ke - kb);
+  // half-tile LDS-DMA: operand X (0 = A, 1 = B), half h, K-tile t -> buffer t & 1; false if t >= nk
+  auto issue = [&](int X, int h, int t) -> bool {
+    if (t >= nk) return false;
+    char* dst = smem + (t & 1) * BUF_BYTES + (X * 2 + h) * HALF_BYTES + wid * 2048;
+    if (X == 0) pa.issue(ra, dst, h, t, klen);
+    else pb.issue(rb, dst, h, t, klen);
+    return true;
+  };
+  auto wait_dma = [&](bool younger_issued) {
+    if (younger_issued) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  bf16x8 af[4][2], blo[2][2], bhi[2][2];
+  auto read_a = [&](int buf, int ih) {  // A rows ih*64 .. +64 of this wave's 128
+    const char* base = smem + buf * BUF_BYTES + wr * HALF_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag<ALAY>(base, ih * 64 + i * 16, kk, lane);
+    if (TN && do_rs) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) rs[ih * 4 + i] = frag_rowsum(af[i][kk], rs[ih * 4 + i]);
+    }
+  };
+  auto read_b = [&](int buf, int jh, bf16x8 (&bf)[2][2]) {  // B cols jh*32 .. +32 of this wave's 64
+    const char* base = smem + buf * BUF_BYTES + (2 + (wc >> 1)) * HALF_BYTES;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = frag<BLAY>(base, (wc & 1) * 64 + jh * 32 + j * 16, kk, lane);
+  };
+  auto mma = [&](int ih, int jh, bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ih * 4 + i][jh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: K-tile 0 (all four halves) and B0 of K-tile 1
+  issue(0, 0, 0);
+  issue(0, 1, 0);
+  issue(1, 0, 0);
+  issue(1, 1, 0);
+  wait_dma(issue(1, 0, 1));
+  bar_raw();
+  if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
+
+  for (int t = 0; t < nk; t += 2) {
+    const bool two = t + 1 < nk;  // second K-tile of this iteration exists
+    // ---- K-tile t (buffer 0) ----
+    read_a(0, 0);
+    read_b(0, 0, blo);
+    issue(1, 1, t + 1);
+    bar_raw();
+    mma(0, 0, blo);
+    bar_raw();
+
+    read_b(0, 1, bhi);
+    issue(0, 0, t + 1);
+    bar_raw();
+    mma(0, 1, bhi);
+    bar_raw();
+
+    read_a(0, 1);
+    issue(0, 1, t + 1);
+    bar_raw();
+    mma(1, 1, bhi);
+    bar_raw();
+
+    wait_dma(issue(1, 0, t + 2));
+    bar_raw();
+    mma(1, 0, blo);
+    bar_raw();
+
+    // ---- K-tile t+1 (buffer 1) ----
+    if (two) {
+      read_a(1, 0);
+      read_b(1, 0, blo);
+    }
+    issue(1, 1, t + 2);
+    bar_raw();
+    if (two) mma(0, 0, blo);
+    bar_raw();
+
+    if (two) read_b(1, 1, bhi);
+    issue(0, 0, t + 2);
+    bar_raw();
+    if (two) mma(0, 1, bhi);
+    bar_raw();
+
+    if (two) read_a(1, 1);
+    issue(0, 1, t + 2);
+    bar_raw();
+    if (two) mma(1, 1, bhi);
+    bar_raw();
+
+    wait_dma(issue(1, 0, t + 3));
+    bar_raw();
+    if (two) mma(1, 0, blo);
+    bar_raw();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wr == 0) bar_raw();  // re-align the groups
+  bar_raw();
+
+  if (do_rs) {
+    float* dst = ksplit > 1 ? ws + (long)ksplit * M * N + (long)split * M : rowsum;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v = rs[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      const long r = m0 + wr * 128 + i * 16 + (lane & 15);
+      if (lane < 16 && r < M) dst[r] = v;
+    }
+  }
+
+  // ---- epilogue: per wave, two passes of 64 rows x 64 cols through a private fp32 LDS stage ----
+  float* cs = (float*)smem + wid * 64 * EPI_LD;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          cs[(i * 16 + (lane >> 4) * 4 + t) * EPI_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][t];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int id = it * 64 + lane;
+      const int r = id >> 3, c8 = (id & 7) * 8;
+      const long gr = m0 + wr * 128 + pass * 64 + r, gc = n0 + wc * 64 + c8;
+      if (gr >= M || gc >= N) continue;
+      const f32x4 lo = *(const f32x4*)(cs + r * EPI_LD + c8), hi = *(const f32x4*)(cs + r * EPI_LD + c8 + 4);
+      if (ksplit > 1) {
+        f32x4* o = (f32x4*)(ws + ((long)split * M + gr) * N + gc);
+        o[0] = lo;
+        o[1] = hi;
+        continue;
+      }
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      epi_row8<ACT, DROP>(e, C, ldc, N, gr, gc, v);
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -490,28 +740,108 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   }
 }
 
-template <int AL, int BL>
+// ------------------------------------------------------------------------------------------------
+// host side: kernel / epilogue-instance selection
+// ------------------------------------------------------------------------------------------------
+template <typename KernelT>
+void set_lds(KernelT k, int bytes) {
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+template <int AL, int BL, int ACT, bool DROP>
 void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, int ksplit, long kchunk,
                  hipStream_t s) {
   const long nbm = (g->M + BM - 1) / BM, nbn = (g->N + BN - 1) / BN;
-  static const int glds = getenv("MIT_GEMM_GLDS") ? atoi(getenv("MIT_GEMM_GLDS")) : 1;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<AL, BL, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              SMEM_BYTES);
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<AL, BL, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              SMEM_BYTES);
+    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP>, SMEM_BYTES);
     attr = true;
   }
-  if (glds)
-    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, true>), dim3((unsigned)(nbm * nbn * ksplit)), dim3(256), SMEM_BYTES, s,
-                       (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                       b_bytes, e, ksplit, kchunk, (float*)g->workspace, g->rowsum);
-  else
-    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, false>), dim3((unsigned)(nbm * nbn * ksplit)), dim3(256), SMEM_BYTES,
-                       s, (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                       b_bytes, e, ksplit, kchunk, (float*)g->workspace, g->rowsum);
+  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP>), dim3((unsigned)(nbm * nbn * ksplit)), dim3(256), SMEM_BYTES,
+                     s, (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                     b_bytes, e, ksplit, kchunk, (float*)g->workspace, g->rowsum);
 }
+
+template <int AL, int BL, int ACT, bool DROP>
+void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  const long nbm = (g->M + B2 - 1) / B2, nbn = (g->N + B2 - 1) / B2;
+  static bool attr = false;
+  if (!attr) {
+    set_lds(gemm256_kernel<AL, BL, ACT, DROP>, SMEM2_BYTES);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP>), dim3((unsigned)(nbm * nbn)), dim3(512), SMEM2_BYTES, s,
+                     (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                     b_bytes, e, 1, g->K, (float*)g->workspace, g->rowsum);
+}
+
+// 0 = pick per shape, 1 = always the 128x128 kernel, 2 = the 256x256 kernel wherever it has an
+// instance for the epilogue (tuning / tests)
+int g_variant = -1;
+int gemm_variant() {
+  if (g_variant < 0) g_variant = getenv("MIT_GEMM_VARIANT") ? atoi(getenv("MIT_GEMM_VARIANT")) : 0;
+  return g_variant;
+}
+
+// Occupancy-quantised cost model: the 128x128 kernel runs 2 blocks per CU, the 256x256 kernel 1;
+// a "round" fills every slot once, and a round of the 256 kernel moves 4 tiles' worth of 128x128
+// work per CU-slot at REL256 x the 128 kernel's per-FLOP speed (tools/gemm_bench.py).
+bool use_256(long M, long N, long K, int a_layout) {
+  const int v = gemm_variant();
+  if (v == 1) return false;
+  if (v == 2) return true;
+  // the MN-contig-A instances (weight gradients) exceed 256 VGPRs and spill: 128 kernel (+ split-K)
+  if (a_layout != MIT_K_CONTIG) return false;
+  if (M < 256 || N < 256 || K < 128) return false;
+  const double REL256 = 1.3, CUS = 256.0;
+  const double t128 = (double)(((M + 127) / 128) * ((N + 127) / 128));
+  const double t256 = (double)(((M + 255) / 256) * ((N + 255) / 256));
+  const double c128 = std::ceil(t128 / (2 * CUS));             // rounds of 2 concurrent 128-tiles per CU
+  const double c256 = std::ceil(t256 / CUS) * 2.0 / REL256;    // one 256-tile = 4 128-tiles on 1 slot of 2
+  return c256 < c128;
+}
+
+// epilogue instance for a bf16 GEMM: {act, dropout} as template parameters where an instance
+// exists (the combinations the train step uses), else the generic run-time instance
+enum EpiKind { EK_PLAIN, EK_RELU, EK_RELU_DROP, EK_GELU, EK_QGELU, EK_GENERIC };
+EpiKind epi_kind(const mit_gemm_args* g) {
+  const bool drop = g->drop_p > 0.f;
+  if (g->act == MIT_ACT_NONE && !drop) return EK_PLAIN;
+  if (g->a_layout != MIT_K_CONTIG || g->b_layout != MIT_K_CONTIG) return EK_GENERIC;
+  if (g->act == MIT_ACT_RELU) return drop ? EK_RELU_DROP : EK_RELU;
+  if (drop) return EK_GENERIC;
+  return g->act == MIT_ACT_GELU ? EK_GELU : EK_QGELU;
+}
+
+template <int AL, int BL>
+void launch_layout(const mit_gemm_args* g, const Epi& e, int ab, int bb, int ks, long kchunk, bool big, hipStream_t s) {
+  const EpiKind k = epi_kind(g);
+  if (big && k != EK_GENERIC) {
+    if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
+      switch (k) {
+        case EK_RELU: return launch_bf16_256<AL, BL, MIT_ACT_RELU, false>(g, e, ab, bb, s);
+        case EK_RELU_DROP: return launch_bf16_256<AL, BL, MIT_ACT_RELU, true>(g, e, ab, bb, s);
+        case EK_GELU: return launch_bf16_256<AL, BL, MIT_ACT_GELU, false>(g, e, ab, bb, s);
+        case EK_QGELU: return launch_bf16_256<AL, BL, MIT_ACT_QUICK_GELU, false>(g, e, ab, bb, s);
+        default: break;
+      }
+    }
+    return launch_bf16_256<AL, BL, MIT_ACT_NONE, false>(g, e, ab, bb, s);
+  }
+  if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
+    switch (k) {
+      case EK_PLAIN: return launch_bf16<AL, BL, MIT_ACT_NONE, false>(g, e, ab, bb, ks, kchunk, s);
+      case EK_RELU: return launch_bf16<AL, BL, MIT_ACT_RELU, false>(g, e, ab, bb, ks, kchunk, s);
+      case EK_RELU_DROP: return launch_bf16<AL, BL, MIT_ACT_RELU, true>(g, e, ab, bb, ks, kchunk, s);
+      case EK_GELU: return launch_bf16<AL, BL, MIT_ACT_GELU, false>(g, e, ab, bb, ks, kchunk, s);
+      case EK_QGELU: return launch_bf16<AL, BL, MIT_ACT_QUICK_GELU, false>(g, e, ab, bb, ks, kchunk, s);
+      default: return launch_bf16<AL, BL, ACT_RT, true>(g, e, ab, bb, ks, kchunk, s);
+    }
+  }
+  if (k == EK_PLAIN) return launch_bf16<AL, BL, MIT_ACT_NONE, false>(g, e, ab, bb, ks, kchunk, s);
+  return launch_bf16<AL, BL, ACT_RT, true>(g, e, ab, bb, ks, kchunk, s);
+}
+
 template <int AL, int BL>
 void launch_f32(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
   dim3 grid((unsigned)((g->N + 63) / 64), (unsigned)((g->M + 63) / 64));
@@ -523,7 +853,11 @@ inline bool al16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 
 }  // namespace
 
-
+extern "C" int mit_gemm_set_variant(int v) {
+  MIT_CHECK_ARG(v >= 0 && v <= 2, "mit_gemm_set_variant: %d not in {0,1,2}", v);
+  g_variant = v;
+  return MIT_OK;
+}
 
 extern "C" long mit_gemm_workspace_bytes(long M, long N, long K) {
   long kc;
@@ -537,6 +871,7 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   MIT_CHECK_ARG(g->A && g->B && g->C, "mit_gemm: null operand");
   MIT_CHECK_ARG(g->a_layout == MIT_K_CONTIG || g->a_layout == MIT_MN_CONTIG, "mit_gemm: bad a_layout");
   MIT_CHECK_ARG(g->b_layout == MIT_K_CONTIG || g->b_layout == MIT_MN_CONTIG, "mit_gemm: bad b_layout");
+  MIT_CHECK_ARG(g->act >= MIT_ACT_NONE && g->act <= MIT_ACT_QUICK_GELU, "mit_gemm: bad act %d", g->act);
   if (g->M == 0 || g->N == 0) return MIT_OK;
   MIT_CHECK_ARG(g->lda >= (g->a_layout == MIT_K_CONTIG ? g->K : g->M), "mit_gemm: lda too small");
   MIT_CHECK_ARG(g->ldb >= (g->b_layout == MIT_K_CONTIG ? g->K : g->N), "mit_gemm: ldb too small");
@@ -585,15 +920,16 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
     if (plain && g->workspace) {
       ks = splitk_plan(g->M, g->N, g->K, &kchunk);
       if (ks > 1 && (splitk_ws_bytes(g->M, g->N, ks) > g->workspace_bytes || !al16(g->workspace) ||
-                     (g->out_f32 ? false : (g->ldc % 4 != 0)) || g->ldc % 4 != 0 || !al16(g->C))) {
+                     g->ldc % 4 != 0 || !al16(g->C))) {
         ks = 1;
         kchunk = g->K;
       }
     }
-    if (g->a_layout == 0 && g->b_layout == 0) launch_bf16<0, 0>(g, e, ab, bb, ks, kchunk, s);
-    else if (g->a_layout == 0 && g->b_layout == 1) launch_bf16<0, 1>(g, e, ab, bb, ks, kchunk, s);
-    else if (g->a_layout == 1 && g->b_layout == 0) launch_bf16<1, 0>(g, e, ab, bb, ks, kchunk, s);
-    else launch_bf16<1, 1>(g, e, ab, bb, ks, kchunk, s);
+    const bool big = ks == 1 && use_256(g->M, g->N, g->K, g->a_layout);
+    if (g->a_layout == 0 && g->b_layout == 0) launch_layout<0, 0>(g, e, ab, bb, ks, kchunk, big, s);
+    else if (g->a_layout == 0 && g->b_layout == 1) launch_layout<0, 1>(g, e, ab, bb, ks, kchunk, big, s);
+    else if (g->a_layout == 1 && g->b_layout == 0) launch_layout<1, 0>(g, e, ab, bb, ks, kchunk, big, s);
+    else launch_layout<1, 1>(g, e, ab, bb, ks, kchunk, big, s);
     if (ks > 1) {
       MIT_LAUNCH_CHECK("mit_gemm");
       const long total = g->M * (g->N / 4);

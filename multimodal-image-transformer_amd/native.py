@@ -63,6 +63,7 @@ SIGNATURES = {
     "mit_abi_version": (I, []),
     "mit_gemm": (I, [ctypes.POINTER(GemmArgs), vp]),
     "mit_gemm_workspace_bytes": (L, [L, L, L]),
+    "mit_gemm_set_variant": (I, [I]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
@@ -87,11 +88,13 @@ SIGNATURES = {
 }
 
 
-def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load the HIP library and declare every signature. Raises if the file is missing."""
+def load_library(path: str = None) -> ctypes.CDLL:
+    """Load the HIP library and declare every signature. Raises if the file is missing.
+    MIT_LIB overrides the in-tree path (A/B builds of the same sources, tools/build_variants.sh)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("MIT_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise NativeError(f"libmit_hip.so not found at {path}: build it with `python __graft_entry__.py build` "
                           f"(or `make -C multimodal-image-transformer_amd/csrc`). There is no CPU fallback.")
@@ -185,6 +188,11 @@ def set_gemm_probe(probe):
     every GEMM launch (bench.py records HIP events there to time the GEMM kernels in place)."""
     global _gemm_probe
     _gemm_probe = probe
+
+
+def gemm_set_variant(v):
+    """0 = per-shape tile-kernel choice, 1 = 128x128 only, 2 = 256x256 wherever legal."""
+    _check(lib().mit_gemm_set_variant(int(v)), "mit_gemm_set_variant")
 
 
 def gemm_workspace_bytes(M, N, K):

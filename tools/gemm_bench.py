@@ -14,34 +14,60 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("dec fc_out", 4032, 10000, 512, 0, 0), ("dX fc_out", 4032, 512, 10000, 0, 1), ("dW fc_out", 10000, 512, 4032, 1, 1),
     ("dW kv_all", 6144, 512, 12608, 1, 1), ("dX kv_all", 12608, 512, 6144, 0, 1), ("dW ffn1", 2048, 512, 4032, 1, 1),
     ("4096^3", 4096, 4096, 4096, 0, 0),
+    ("enc fc1+gelu", 12608, 3072, 768, 0, 0, "gelu"), ("enc fc2+res", 12608, 768, 3072, 0, 0, "res"),
+    ("enc qkv+bias", 12608, 2304, 768, 0, 0, "bias"), ("dec ffn1+relu+drop", 4032, 2048, 512, 0, 0, "reludrop"),
 ]
 
 
-def run(iters=20):
+def run(iters=20, variants=(1, 2)):
     torch.manual_seed(0)
     dev = torch.device("cuda")
     res = []
-    for name, M, N, K, al, bl in SHAPES:
+    only = os.environ.get("GEMM_SHAPES")
+    for name, M, N, K, al, bl, *epi in SHAPES:
+        if only and name not in only.split(","):
+            continue
+        epi = epi[0] if epi else ""
         A = (torch.randn(M, K) if al == 0 else torch.randn(K, M)).to(dev, torch.bfloat16)
         B = (torch.randn(N, K) if bl == 0 else torch.randn(K, N)).to(dev, torch.bfloat16)
         out_f32 = al == 1
         C = torch.empty(M, N, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
-        for _ in range(3):
-            native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(iters):
-            native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl)
-        e1.record()
-        torch.cuda.synchronize()
-        t = e0.elapsed_time(e1) / iters * 1e-3
-        tf = 2 * M * N * K / t / 1e12
-        res.append((name, M, N, K, t * 1e6, tf))
-        print(f"{name:12s} {M:6d} {N:6d} {K:6d} {al}{bl}  {t*1e6:9.1f} us  {tf:7.1f} TFLOP/s", flush=True)
+        kw = {}
+        if epi:
+            kw["bias"] = torch.randn(N, device=dev)
+        if epi == "gelu":
+            kw["act"] = native.ACT_GELU
+        if epi == "res":
+            kw["residual"] = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        if epi == "reludrop":
+            kw.update(act=native.ACT_RELU, drop_p=0.1, seed=torch.tensor([7], device=dev), site=1)
+        best = {}
+        for rnd in range(3):  # interleaved rounds, one process (guide §5.4 rule 24)
+            for v in variants:
+                native.gemm_set_variant(v)
+                for _ in range(3):
+                    native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, **kw)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(iters):
+                    native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, **kw)
+                e1.record()
+                torch.cuda.synchronize()
+                t = e0.elapsed_time(e1) / iters * 1e-3
+                best[v] = min(best.get(v, 1e9), t)
+        line = f"{name:12s} {M:6d} {N:6d} {K:6d} {al}{bl}"
+        for v in variants:
+            t = best[v]
+            tf = 2 * M * N * K / t / 1e12
+            res.append((name, v, M, N, K, t * 1e6, tf))
+            line += f"  v{v} {t*1e6:8.1f} us {tf:7.1f} TF"
+        print(line, flush=True)
+    native.gemm_set_variant(0)
     return res
 
 
 if __name__ == "__main__":
     native.load_library()
-    run()
+    vs = tuple(int(v) for v in sys.argv[1].split(",")) if len(sys.argv) > 1 else (1, 2)
+    run(variants=vs)
