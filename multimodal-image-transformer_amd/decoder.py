@@ -22,6 +22,7 @@ MI355X-specific layout decisions:
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
@@ -168,6 +169,48 @@ class _Acts:
                       (R, d, V), (B * S, d, L * 2 * d)]
             need = max(native.gemm_workspace_bytes(m, n, k) for m, n, k in shapes)
             self.gemm_ws = torch.empty(max(need, 16) // 4 + 4, dtype=torch.float32, device=dev)
+            # the weight-gradient GEMMs run on a side stream (_SideStream) with their own scratch
+            self.gemm_ws_side = torch.empty(max(need, 16) // 4 + 4, dtype=torch.float32, device=dev)
+
+
+class _SideStream:
+    """Second HIP stream for the backward's weight-gradient GEMMs (dW = dY^T X). Each layer's dW
+    and dX GEMMs are independent; at d = 512 a decoder GEMM fills only 128-512 of the CUs' 512
+    block slots, so running the dW chain beside the main dX -> LayerNorm -> attention chain fills
+    the machine. Ordering: side waits for main before each dW (its dY is final); main waits for the
+    side's last reader of a gradient buffer before overwriting it (guard); join() at the end. All
+    edges are HIP events, so the step still captures into ONE hipGraph (as parallel branches)."""
+
+    def __init__(self, device):
+        self.stream = torch.cuda.Stream(device=device)
+        self.pending = {}
+
+    def run(self, fn, reads=()):
+        main = torch.cuda.current_stream()
+        self.stream.wait_stream(main)
+        with torch.cuda.stream(self.stream):
+            fn()
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        for t in reads:
+            self.pending[t.data_ptr()] = ev
+
+    def guard(self, t):
+        """Before the main stream writes t: wait for the side-stream GEMM still reading it."""
+        ev = self.pending.pop(t.data_ptr(), None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+
+    def under(self, fn):
+        """Run fn (e.g. a DP gradient-bucket all-reduce) on the side stream after everything issued
+        so far on both streams."""
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            fn()
+
+    def join(self):
+        torch.cuda.current_stream().wait_stream(self.stream)
+        self.pending.clear()
 
 
 class TransformerDecoder:
@@ -199,6 +242,9 @@ class TransformerDecoder:
         self.pe = sinusoidal_pe(max_seq_len, embed_dim).to(self.device)
         self.training = True
         self._acts: Dict[tuple, _Acts] = {}
+        # weight-gradient GEMMs on a second stream (MIT_DW_SIDE_STREAM=0 disables, for A/B)
+        self.dw_side_stream = os.environ.get("MIT_DW_SIDE_STREAM", "1") != "0"
+        self._side = None
         if self._own_store:
             self.init_weights(0)
 
@@ -242,6 +288,11 @@ class TransformerDecoder:
 
     def eval(self):
         return self.train(False)
+
+    def _side_stream(self) -> "_SideStream":
+        if self._side is None:
+            self._side = _SideStream(self.device)
+        return self._side
 
     # --- forward -----------------------------------------------------------------------------
     def acts(self, B, T, S, train) -> _Acts:
@@ -322,17 +373,34 @@ class TransformerDecoder:
         MN, K = native.MN_CONTIG, native.K_CONTIG
         x_last = A.xs[L - 1][2]
         ws = A.gemm_ws
+        side = self._side_stream() if self.dw_side_stream else None
 
         def dW(dy, x, wname, bname, M, N, K, lda, ldb):
-            """weight grad dY^T X (TN GEMM) with the bias grad (row sums of dY^T) fused in, split-K."""
-            native.gemm(dy, x, g(wname), M, N, K, a_layout=MN, b_layout=MN, lda=lda, ldb=ldb, rowsum=g(bname),
-                        workspace=ws)
+            """weight grad dY^T X (TN GEMM) with the bias grad (row sums of dY^T) fused in, split-K;
+            on the side stream when enabled."""
+            if side is None:
+                native.gemm(dy, x, g(wname), M, N, K, a_layout=MN, b_layout=MN, lda=lda, ldb=ldb, rowsum=g(bname),
+                            workspace=ws)
+                return
+            side.run(lambda: native.gemm(dy, x, g(wname), M, N, K, a_layout=MN, b_layout=MN, lda=lda, ldb=ldb,
+                                         rowsum=g(bname), workspace=A.gemm_ws_side), reads=(dy,))
+
+        def guard(t):
+            if side is not None:
+                side.guard(t)
+
+        def ready(first, last):
+            if grads_ready is None:
+                return
+            if side is None:
+                grads_ready(first, last)
+            else:
+                side.under(lambda: grads_ready(first, last))
 
         # fc_out
         dW(dlogits, x_last, "fc_out.weight", "fc_out.bias", V, d, R, V, d)
         native.gemm(dlogits, w("fc_out.weight"), A.dx, R, d, V, b_layout=MN, ldb=d, workspace=ws)
-        if grads_ready:
-            grads_ready("fc_out.weight", "fc_out.bias")
+        ready("fc_out.weight", "fc_out.bias")
         ascale = 1.0 / (1.0 - p) if p > 0 else 1.0
         for l in reversed(range(L)):
             pre = f"layers.{l}."
@@ -340,16 +408,19 @@ class TransformerDecoder:
             xs, z, stt = A.xs[l], A.z[l], A.st[l]
             xin = A.x0 if l == 0 else A.xs[l - 1][2]
             # LN3 -> dz3 (dx, in place) and d(ffn_out) (dy)
+            guard(A.dy)
             native.layernorm_bwd(A.dx, z[2], stt[2][0], stt[2][1], st.p(pre + "norm3.weight"), A.dx,
                                  g(pre + "norm3.weight"), g(pre + "norm3.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
                                  site=base + 5)
             # FFN
             dW(A.dy, A.h[l], pre + "linear2.weight", pre + "linear2.bias", d, F, R, d, F)
+            guard(A.dh)
             native.gemm(A.dy, w(pre + "linear2.weight"), A.dh, R, F, d, b_layout=MN, ldb=F, aux=A.h[l], ld_aux=F,
                         aux_scale=ascale)
             dW(A.dh, xs[1], pre + "linear1.weight", pre + "linear1.bias", F, d, R, F, d)
             native.gemm(A.dh, w(pre + "linear1.weight"), A.dx, R, d, F, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
             # LN2
+            guard(A.dy)
             native.layernorm_bwd(A.dx, z[1], stt[1][0], stt[1][1], st.p(pre + "norm2.weight"), A.dx,
                                  g(pre + "norm2.weight"), g(pre + "norm2.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
                                  site=base + 3)
@@ -362,10 +433,12 @@ class TransformerDecoder:
                                   seed=seed, site=base + 2)
             cg = native.attn_grads(A.do, d, T * d, A.dq, d, T * d, dkvl, L * 2 * d, S * L * 2 * d, dkvl[:, d:],
                                    L * 2 * d, S * L * 2 * d, A.delta)
+            guard(A.dq)
             native.attention_bwd(native.dtype_code(A.dq), B, H, T, S, ca, cg)
             dW(A.dq, xs[0], pre + "cross_q.weight", pre + "cross_q.bias", d, d, R, d, d)
             native.gemm(A.dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
             # LN1
+            guard(A.dy)
             native.layernorm_bwd(A.dx, z[0], stt[0][0], stt[0][1], st.p(pre + "norm1.weight"), A.dx,
                                  g(pre + "norm1.weight"), g(pre + "norm1.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
                                  site=base + 1)
@@ -379,11 +452,11 @@ class TransformerDecoder:
                                   site=base + 0)
             sg = native.attn_grads(A.do, d, T * d, A.dqkv, 3 * d, T * 3 * d, A.dqkv[:, d:], 3 * d, T * 3 * d,
                                    A.dqkv[:, 2 * d:], 3 * d, T * 3 * d, A.delta)
+            guard(A.dqkv)
             native.attention_bwd(native.dtype_code(A.dq), B, H, T, T, sa, sg)
             dW(A.dqkv, xin, pre + "self_in.weight", pre + "self_in.bias", 3 * d, d, R, 3 * d, d)
             native.gemm(A.dqkv, w(pre + "self_in.weight"), A.dx, R, d, 3 * d, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
-            if grads_ready:
-                grads_ready(pre + "linear2.weight", pre + "norm1.bias")
+            ready(pre + "linear2.weight", pre + "norm1.bias")
         # cross K/V of all layers
         BS = B * S
         dW(A.dkv, mem, "cross_kv.weight", "cross_kv.bias", L * 2 * d, d, BS, L * 2 * d, mem_ld)
@@ -397,8 +470,9 @@ class TransformerDecoder:
             native.gemm(A.dkv, w("cross_kv.weight"), A.dmem, BS, d, L * 2 * d, b_layout=MN, ldb=d, workspace=ws)
             dW(A.dmem, enc_rows, "projection.weight", "projection.bias", d, E, BS, d, enc_ld)
             last = "projection.bias"
-        if grads_ready:
-            grads_ready("cross_kv.weight", last)
+        ready("cross_kv.weight", last)
+        if side is not None:
+            side.join()
 
     def forward(self, tgt_tokens: torch.Tensor, memory: torch.Tensor, memory_padding_mask=None) -> torch.Tensor:
         """decoder.py:134-193: f32 logits [B, T, V] (no autograd; training goes through the model's
