@@ -212,6 +212,39 @@ def cpu_baseline(model, args):
                       f"median of {args.cpu_steps} steps after 1 warm-up, dropout off; cpu: {cpu_model}"}
 
 
+def bench_decode(args):
+    """configs[4]: greedy captions for a batch of images (ImageToTextModel.generate_batch). END is set
+    to an id the vocabulary never produces, so every caption runs the full max_len - 1 tokens (fixed
+    work per call). One call = encoder forward + cross K/V + (max_len - 1) replayed token steps."""
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    args.memory_mode = "patches"
+    model, _ = build(args, 0)
+    model.eval()
+    B = args.decode_batch
+    images = synthetic_batch(B, 2, args.vocab, dev, 5)[0]
+    never = args.vocab + 7
+    for _ in range(max(1, args.warmup // 2)):
+        model.generate_batch(images, 2, never, max_len=args.max_len)
+    torch.cuda.synchronize()
+    K = max(1, args.steps // 4)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        ids = model.generate_batch(images, 2, never, max_len=args.max_len)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    toks = B * (args.max_len - 1) * K
+    out = {"metric": "greedy caption tokens/sec (batched KV-cache decode, 6L/d512 decoder + ViT-B/16)",
+           "value": round(toks / el, 1), "unit": "tokens/s", "n_gpus": 1, "steps": K, "warmup": max(1, args.warmup // 2),
+           "ms_per_step": round(1e3 * el / K, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": args.dtype, "data": "synthetic (randn 224x224 images; random-init weights)",
+           "config": {"workload": "configs[4]: inference.py greedy decode, cached cross-attn K/V, hipGraph-captured "
+                                  "per-token step", "images": B, "max_len": args.max_len, "memory_mode": "patches"},
+           "images_per_s": round(B * K / el, 2), "us_per_token_step": round(1e6 * el / K / (args.max_len - 1), 2),
+           "ids_per_caption": len(ids[0])}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -232,7 +265,14 @@ def main():
                          "weight-gradient stream run beside the main stream (measured faster than the graph, whose "
                          "parallel branches ROCm 7 does not overlap)")
     ap.add_argument("--no-graph", action="store_true", help="(default; kept for older scripts)")
+    ap.add_argument("--workload", default="train", choices=["train", "decode"],
+                    help="train: the BASELINE metric (default). decode: configs[4], batched greedy captioning "
+                         "(KV cache, hipGraph-replayed token step)")
+    ap.add_argument("--decode-batch", type=int, default=256)
+    ap.add_argument("--max-len", type=int, default=100, help="decode: ids per caption (config.MAX_SEQ_LEN)")
     args = ap.parse_args()
+    if args.workload == "decode":
+        return bench_decode(args)
 
     from dist import DataParallel, init_from_env
     import torch.distributed as tdist

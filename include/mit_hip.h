@@ -207,6 +207,33 @@ int mit_adamw(long n, float* param, const float* grad, float* m, float* v, void*
               void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Batched greedy decoding with a KV cache (BASELINE config 5). Replaces the per-token full-prefix
+ * recompute of ImageToTextModel.generate (model.py:171-242: decoder forward over ids[0..t], argmax
+ * of the last position, stop at END) by one cached step per token for a whole batch. Every position
+ * is read from the DEVICE scalar `pos` (int64), so one step captures into a hipGraph and replays.
+ *
+ * attention_decode: o[b, h*64:(h+1)*64] = softmax(q_bh . K_bh^T * scale) V_bh for ONE query per
+ *   (b, h); keys j < Lk with Lk = *pos + 1 when pos != NULL (causal self-attention over the cache),
+ *   else the fixed Lk (cross-attention over the image memory). Key j is masked when
+ *   key_tokens[b*tok_batch + j] == pad_idx (the reference's key-padding mask, utils.py:47-70), when
+ *   key_tokens != NULL. Head dim 64, heads at column h*64 of each row. All keys masked -> NaN.
+ * kv_store: cache[b*c_batch + (*pos)*c_row + e] = src[b*s_batch + e], e < n.
+ * embed_decode: out[b, :] = table[ids[b*ld_ids + *pos]] * scale + pe[*pos]   (decoder.py:168-171)
+ * greedy_pick: ids[b*ld_ids + *pos + 1] = argmax_v logits[b*ld + v] (first maximal index, like
+ *   torch.argmax, model.py:236) for rows not yet finished (finished rows get pad_id); a row whose
+ *   pick is end_id sets finished[b] = 1 and increments *n_finished (int32 device scalars). */
+int mit_attention_decode(int dtype, long B, long H, const void* q, long q_batch, const void* k, long k_row,
+                         long k_batch, const void* v, long v_row, long v_batch, void* o, long o_batch, long Lk,
+                         const int64_t* pos, const int64_t* key_tokens, long tok_batch, int pad_idx, float scale,
+                         void* stream);
+int mit_kv_store(int dtype, long B, long n, const void* src, long s_batch, void* cache, long c_row, long c_batch,
+                 const int64_t* pos, void* stream);
+int mit_embed_decode(int dtype, long B, long d, const int64_t* ids, long ld_ids, const int64_t* pos, const void* table,
+                     float scale, const float* pe, void* out, void* stream);
+int mit_greedy_pick(long B, long V, const float* logits, long ld, int64_t* ids, long ld_ids, const int64_t* pos,
+                    int64_t end_id, int64_t pad_id, int* finished, int* n_finished, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Utilities. cast: f32 -> operand dtype copy (weights to the bf16 shadow); fill f32.
  * dropout_mask_debug: writes the keep-multiplier (0 or 1/(1-p)) the kernels use at
  * (seed, site, idx) for idx in [0, n) — tests rebuild reference masks from it. */

@@ -213,6 +213,38 @@ class _SideStream:
         self.pending.clear()
 
 
+class DecodeState:
+    """Device state of a batched greedy decode (TransformerDecoder.decode_begin / decode_step):
+    token ids [B, max_len] (int64; column 0 = START), the device position, per-row finished flags
+    and their count, the cross-attention K/V of all layers [B*S, L*2d], per-layer self-attention
+    caches [B, max_len, 2d] (K | V), and the B-row activations of one token step."""
+
+    def __init__(self, dec: "TransformerDecoder", B: int, S: int, max_len: int, start_id: int, end_id: int):
+        dev, dt = dec.device, dec.dtype
+        d, F, L, V = dec.d, dec.F, dec.L, dec.V
+        self.B, self.S, self.max_len, self.end_id = B, S, max_len, int(end_id)
+        self.ids = torch.full((B, max_len), dec.pad_idx, dtype=torch.int64, device=dev)
+        self.ids[:, 0] = int(start_id)
+        self.pos = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.finished = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.n_finished = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.kv = torch.empty(B * S, L * 2 * d, dtype=dt, device=dev)
+        self.cache = [torch.empty(B, max_len, 2 * d, dtype=dt, device=dev) for _ in range(L)]
+        e = lambda n: torch.empty(B, n, dtype=dt, device=dev)  # noqa: E731
+        self.x, self.x1, self.x2, self.y, self.o, self.q = e(d), e(d), e(d), e(d), e(d), e(d)
+        self.qkv, self.h = e(3 * d), e(F)
+        self.logits = torch.empty(B, V, dtype=torch.float32, device=dev)  # f32: argmax on unrounded logits
+
+    def token_lists(self) -> List[List[int]]:
+        """Per row: START .. up to and including the first END (model.py:236-242), else max_len ids."""
+        out = []
+        for row in self.ids.cpu().tolist():
+            if self.end_id in row[1:]:
+                row = row[: row.index(self.end_id, 1) + 1]
+            out.append(row)
+        return out
+
+
 class TransformerDecoder:
     """Reference-surface decoder: same constructor arguments as decoder.py:84-85.
 
@@ -473,6 +505,52 @@ class TransformerDecoder:
         ready("cross_kv.weight", last)
         if side is not None:
             side.join()
+
+    # --- batched greedy decoding with a KV cache (config 5) ---------------------------------------
+    def decode_begin(self, mem: torch.Tensor, mem_ld: int, S: int, B: int, max_len: int, start_id: int,
+                     end_id: int) -> "DecodeState":
+        """Set up a batched greedy decode over B images whose memory rows are mem [B*S, d] (row
+        stride mem_ld): cross-attention K/V of every layer computed once (one fused GEMM), empty
+        self-attention caches, ids[:, 0] = START, position 0 on the device."""
+        if max_len > self.pe.shape[0]:
+            raise ValueError(f"max_len {max_len} exceeds the positional table ({self.pe.shape[0]} = "
+                             f"decoder_max_seq_len; the reference's PositionalEncoding would fail too)")
+        stt = DecodeState(self, B, S, max_len, start_id, end_id)
+        d, L, st = self.d, self.L, self.store
+        native.gemm(mem, st.w("cross_kv.weight"), stt.kv, B * S, L * 2 * d, d, lda=mem_ld, bias=st.p("cross_kv.bias"))
+        return stt
+
+    def decode_step(self, stt: "DecodeState"):
+        """One greedy token for every row: position p = stt.pos (device) -> ids[:, p+1]; p += 1.
+        No host synchronisation: capturable into a hipGraph."""
+        d, H, L, V = self.d, self.H, self.L, self.V
+        st, w = self.store, self.store.w
+        B, S, Tm = stt.B, stt.S, stt.max_len
+        native.embed_decode(stt.ids, stt.pos, w("token_embedding.weight"), math.sqrt(d), self.pe, stt.x)
+        x = stt.x
+        for l in range(L):
+            pre = f"layers.{l}."
+            cache = stt.cache[l]
+            native.linear(x, w(pre + "self_in.weight"), stt.qkv, bias=st.p(pre + "self_in.bias"))
+            native.kv_store(stt.qkv[:, d:], 3 * d, cache, 2 * d, Tm * 2 * d, B, 2 * d, stt.pos)
+            native.attention_decode(stt.qkv, 3 * d, cache, 2 * d, Tm * 2 * d, cache[:, :, d:], 2 * d, Tm * 2 * d, stt.o,
+                                    d, B, H, pos=stt.pos, key_tokens=stt.ids, tok_batch=Tm, pad_idx=self.pad_idx,
+                                    scale=1.0 / math.sqrt(64))
+            native.linear(stt.o, w(pre + "self_out.weight"), stt.y, bias=st.p(pre + "self_out.bias"))
+            native.layernorm_fwd(x, st.p(pre + "norm1.weight"), st.p(pre + "norm1.bias"), 1e-5, stt.x1, r=stt.y)
+            native.linear(stt.x1, w(pre + "cross_q.weight"), stt.q, bias=st.p(pre + "cross_q.bias"))
+            kvl = stt.kv[:, l * 2 * d:]
+            native.attention_decode(stt.q, d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d, S * L * 2 * d,
+                                    stt.o, d, B, H, Lk=S, scale=1.0 / math.sqrt(64))
+            native.linear(stt.o, w(pre + "cross_out.weight"), stt.y, bias=st.p(pre + "cross_out.bias"))
+            native.layernorm_fwd(stt.x1, st.p(pre + "norm2.weight"), st.p(pre + "norm2.bias"), 1e-5, stt.x2, r=stt.y)
+            native.linear(stt.x2, w(pre + "linear1.weight"), stt.h, bias=st.p(pre + "linear1.bias"),
+                          act=native.ACT_RELU)
+            native.linear(stt.h, w(pre + "linear2.weight"), stt.y, bias=st.p(pre + "linear2.bias"))
+            native.layernorm_fwd(stt.x2, st.p(pre + "norm3.weight"), st.p(pre + "norm3.bias"), 1e-5, x, r=stt.y)
+        native.linear(x, w("fc_out.weight"), stt.logits, bias=st.p("fc_out.bias"))
+        native.greedy_pick(stt.logits, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished, stt.n_finished)
+        native.step_inc(stt.pos)
 
     def forward(self, tgt_tokens: torch.Tensor, memory: torch.Tensor, memory_padding_mask=None) -> torch.Tensor:
         """decoder.py:134-193: f32 logits [B, T, V] (no autograd; training goes through the model's

@@ -282,6 +282,43 @@ class ImageToTextModel:
                 break
         return ids
 
+    @torch.no_grad()
+    def generate_batch(self, images, start_token_id: int, end_token_id: int, max_len: int = 100,
+                       use_graph: bool = True, check_every: int = 8) -> List[List[int]]:
+        """Greedy captions for a whole batch (BASELINE config 5): per image the same token list as
+        generate() (model.py:171-242: START, argmax of the last position each step, stop after END,
+        at most max_len ids), computed with cached self-attention K/V, the cross-attention K/V of
+        the image memory computed once, and ONE hipGraph-captured step replayed per token. The host
+        checks the finished count every `check_every` tokens (the only synchronisation)."""
+        self.eval()
+        pv = images if isinstance(images, torch.Tensor) else \
+            self.image_processor(images=images, return_tensors="pt")["pixel_values"]
+        pv = pv.to(self.device).float()
+        B = pv.shape[0]
+        mem, mem_ld, S, _, _ = self._encode_memory(pv)
+        dec = self.decoder
+        stt = dec.decode_begin(mem, mem_ld, S, B, max_len, start_token_id, end_token_id)
+        steps = max_len - 1
+        if steps <= 0:
+            return stt.token_lists()
+        dec.decode_step(stt)  # position 0 (eager: warms every kernel before capture)
+        done = 1
+        if use_graph and steps > 1:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                dec.decode_step(stt)
+            run = graph.replay
+        else:
+            run = lambda: dec.decode_step(stt)  # noqa: E731
+        while done < steps:
+            n = min(check_every, steps - done)
+            for _ in range(n):
+                run()
+            done += n
+            if int(stt.n_finished.item()) == B:
+                break
+        return stt.token_lists()
+
     # --- checkpoints (reference key names, SURVEY.md §8b) --------------------------------------
     def state_dict(self) -> Dict[str, torch.Tensor]:
         sd = {}

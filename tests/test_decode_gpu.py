@@ -1,0 +1,146 @@
+"""Batched greedy decoding with a KV cache (decode.hip, BASELINE config 5): the decode attention
+kernel against a float64 torch softmax attention (masks, ragged key counts, the all-masked NaN), and
+ImageToTextModel.generate_batch against the reference's own greedy ids (golden fixture) and against
+the per-image full-prefix-recompute generate() (model.py:171-242) in fp32."""
+import math
+
+import pytest
+import torch
+
+import fixtures as FX
+import native as N
+from model_util import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N.load_library()
+
+
+def _ref_attn(q, k, v, lk, key_tokens=None, pad=0):
+    """q [B,H,64], k/v [B,Lmax,H,64] -> o [B,H,64] over keys < lk, PAD keys masked (float64)."""
+    s = torch.einsum("bhd,bjhd->bhj", q.double(), k[:, :lk].double()) / 8.0
+    if key_tokens is not None:
+        s = s.masked_fill((key_tokens[:, :lk] == pad)[:, None, :], float("-inf"))
+    p = torch.softmax(s, -1)
+    return torch.einsum("bhj,bjhd->bhd", p, v[:, :lk].double())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("lk", [1, 7, 33, 64, 197])
+def test_attention_decode_self_with_pad(dtype, lk):
+    B, H, Lmax, d = 5, 8, 200, 512
+    g = torch.Generator().manual_seed(lk)
+    dev = torch.device("cuda")
+    qkv = torch.randn(B, 3 * d, generator=g).to(dev, dtype)
+    cache = torch.randn(B, Lmax, 2 * d, generator=g).to(dev, dtype)
+    toks = torch.randint(1, 50, (B, Lmax), generator=g)
+    toks[0, 0] = 0  # PAD keys: masked like the reference's key-padding mask
+    toks[1, lk // 2] = 0
+    toks_d = toks.to(dev)
+    pos = torch.tensor([lk - 1], dtype=torch.int64, device=dev)
+    o = torch.empty(B, d, device=dev, dtype=dtype)
+    N.attention_decode(qkv, 3 * d, cache, 2 * d, Lmax * 2 * d, cache[:, :, d:], 2 * d, Lmax * 2 * d, o, d, B, H,
+                       pos=pos, key_tokens=toks_d, tok_batch=Lmax, pad_idx=0)
+    q = qkv[:, :d].view(B, H, 64).cpu()
+    k = cache[:, :, :d].reshape(B, Lmax, H, 64).cpu()
+    v = cache[:, :, d:].reshape(B, Lmax, H, 64).cpu()
+    ref = _ref_attn(q, k, v, lk, toks, 0).view(B, d)
+    got = o.double().cpu()
+    # rows whose keys are all PAD (lk == 1: rows 0 and 1) are NaN, like the reference's softmax
+    dead = torch.isnan(ref).any(-1)
+    assert dead.sum().item() == (2 if lk == 1 else 0)
+    assert torch.isnan(got[dead]).all()
+    got, ref = got[~dead], ref[~dead]
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert (got - ref).abs().max().item() < tol
+
+
+def test_attention_decode_cross_fixed_lk():
+    B, H, S, d, L = 4, 8, 197, 512, 3
+    g = torch.Generator().manual_seed(9)
+    dev = torch.device("cuda")
+    q = torch.randn(B, d, generator=g).to(dev)
+    kv = torch.randn(B * S, L * 2 * d, generator=g).to(dev)
+    l = 1
+    kvl = kv[:, l * 2 * d:]
+    o = torch.empty(B, d, device=dev)
+    N.attention_decode(q, d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d, S * L * 2 * d, o, d, B, H, Lk=S)
+    k = kv.view(B, S, L * 2 * d)[:, :, l * 2 * d:l * 2 * d + d].reshape(B, S, H, 64).cpu()
+    v = kv.view(B, S, L * 2 * d)[:, :, l * 2 * d + d:l * 2 * d + 2 * d].reshape(B, S, H, 64).cpu()
+    ref = _ref_attn(q.view(B, H, 64).cpu(), k, v, S).view(B, d)
+    assert (o.double().cpu() - ref).abs().max().item() < 1e-5
+
+
+def test_greedy_pick_first_max_and_end():
+    dev = torch.device("cuda")
+    B, V, T = 3, 1000, 6
+    logits = torch.randn(B, V, device=dev)
+    logits[0, 17] = 50.0
+    logits[0, 900] = 50.0  # tie: the first index wins (torch.argmax)
+    logits[1, 3] = 60.0  # END
+    ids = torch.zeros(B, T, dtype=torch.int64, device=dev)
+    pos = torch.tensor([2], dtype=torch.int64, device=dev)
+    fin = torch.zeros(B, dtype=torch.int32, device=dev)
+    fin[2] = 1
+    nf = torch.zeros(1, dtype=torch.int32, device=dev)
+    N.greedy_pick(logits, ids, pos, 3, 0, fin, nf)
+    ids = ids.cpu()
+    assert ids[0, 3].item() == 17
+    assert ids[1, 3].item() == 3 and fin[1].item() == 1 and nf.item() == 1
+    assert ids[2, 3].item() == 0  # already finished -> PAD
+
+
+def _trained(name, dtype):
+    import optim
+    meta, T = FX.load(name)
+    m, _ = build_model(meta, dtype)
+    m.train()
+    opt = optim.AdamW(m.store, lr=meta["lr"], betas=tuple(meta["betas"]), eps=meta["eps"],
+                      weight_decay=meta["weight_decay"])
+    for s in range(meta["steps"]):
+        imgs, di, tg = FX.inputs(meta, s)
+        m.train_step(imgs.cuda(), di.cuda(), tg.cuda())
+        opt.step(meta["clip_first"] if s == 0 else meta["clip_rest"])
+    return m, meta, T
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_generate_batch_matches_reference_ids(use_graph):
+    """The reference's greedy ids (fixture: model.generate on 2 images after 3 train steps),
+    produced here by ONE batched, KV-cached, graph-replayed decode."""
+    m, meta, T = _trained("tiny_vit_cls", torch.float32)
+    g = meta["generate"]
+    imgs = torch.cat([T["gen.pixel_values0"], T["gen.pixel_values1"]], 0)
+    got = m.generate_batch(imgs, g["start"], g["end"], max_len=g["max_len"], use_graph=use_graph)
+    assert got == [g["ids"][0], g["ids"][1]]
+
+
+@pytest.mark.parametrize("name", ["tiny_vit_patches", "tiny_clip336_patches"])
+def test_generate_batch_matches_full_recompute(name):
+    """Batched KV-cache decode == per-image full-prefix recompute (the reference algorithm) in fp32,
+    over longer captions than the fixture stores (cross-attention over all patches)."""
+    m, meta, _ = _trained(name, torch.float32)
+    img = FX.inputs(meta, 0)[0]
+    imgs = torch.cat([img, img.flip(-1), img * 0.5], 0)
+    batch = m.generate_batch(imgs, 2, 3, max_len=24)
+    for b in range(imgs.shape[0]):
+        single = m.generate(imgs[b:b + 1], 2, 3, max_len=24)
+        assert batch[b] == single, (b, batch[b], single)
+
+
+def test_generate_batch_bf16_agrees_with_fp32():
+    """bf16 decode tracks the fp32 one (same weights): first tokens identical, >= 80 % overall."""
+    m32, meta, _ = _trained("tiny_vit_patches", torch.float32)
+    m16, _, _ = _trained("tiny_vit_patches", torch.bfloat16)
+    img = FX.inputs(meta, 0)[0]
+    a = m32.generate_batch(img, 2, 3, max_len=16)
+    b = m16.generate_batch(img, 2, 3, max_len=16)
+    same = sum(x == y for ra, rb in zip(a, b) for x, y in zip(ra, rb))
+    total = sum(min(len(ra), len(rb)) for ra, rb in zip(a, b))
+    assert all(ra[1] == rb[1] for ra, rb in zip(a, b))
+    assert same >= 0.8 * total
