@@ -444,6 +444,140 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
 }
 
 // ------------------------------------------------------------------------------------------------
+// bf16 MFMA forward, head-resident K/V (no causal / PAD mask: the encoder MHSA and the decoder
+// cross-attention). One workgroup per (b, h) stages the WHOLE K and V of the head in LDS once
+// (Lk rounded up to 32 rows, <= 640 rows = 160 KiB; rows past Lk read as zero and are masked),
+// then NW waves sweep 16-query tiles (ceil(Lq/16) tiles, so L = 197 wastes 5 % instead of the 30 %
+// of 64-query blocks) against 32-key chunks with no barrier, no global load and no LDS write inside
+// the key loop. Per chunk and wave: S^T = K Q^T (4 MFMAs) -> online softmax on 8 in-lane scores ->
+// O^T += V^T P^T (4 MFMAs, P straight from the accumulators, same permutation as attn_fwd_mfma).
+// Dropout (decoder cross-attention in training) is a template flag.
+// ------------------------------------------------------------------------------------------------
+constexpr int HK_MAX = 640;  // keys per head the LDS can hold (K + V = 256 B per key)
+
+template <bool DROP>
+__global__ __launch_bounds__(1024) void attn_fwd_head(long H, long Lq, long Lk, AttnK a, int kbytes, int vbytes,
+                                                      int lkp) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* Ks = lds;
+  char* Vs = lds + (long)lkp * 128;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, nw = blockDim.x >> 6;
+  const long h = blockIdx.x, b = blockIdx.y;
+  const bf16* Kb = (const bf16*)a.k + b * a.k_batch + h * D;
+  const bf16* Vb = (const bf16*)a.v + b * a.v_batch + h * D;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, kbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, vbytes, 0x00020000);
+  // stage K and V: 8 16-B chunks per row
+  for (int id = tid; id < lkp * 8; id += blockDim.x) {
+    const int r = id >> 3, c = id & 7;
+    const bool ok = r < Lk;
+    const u32x4 kv = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rk, (int)(ok ? (uint32_t)((r * a.k_row + c * 8) * 2) : A_OOB), 0, 0));
+    const u32x4 vv = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rv, (int)(ok ? (uint32_t)((r * a.v_row + c * 8) * 2) : A_OOB), 0, 0));
+    *(u32x4*)(Ks + koff_k(r, c)) = kv;
+    *(u32x4*)(Vs + koff_v(r, c * 16)) = vv;
+  }
+  __syncthreads();
+
+  const float sl2 = a.scale * 1.4426950408889634f;  // scores in log2 units
+  const uint64_t key = DROP ? site_key(a.seed, a.site) : 0ull;
+  const int nqt = (int)((Lq + 15) / 16);
+  const int q = (lane & 15) >> 2, pp = lane & 3;
+  for (int qt = w; qt < nqt; qt += nw) {
+    const long qi = (long)qt * 16 + (lane & 15);
+    const bool qlive = qi < Lq;
+    bf16x8 qf[2];
+    {
+      const bf16* Qr = (const bf16*)a.q + b * a.q_batch + h * D + (qlive ? qi : 0) * a.q_row;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        u32x4 v = *(const u32x4*)(Qr + kk * 32 + g * 8);
+        if (!qlive) v = u32x4{0u, 0u, 0u, 0u};
+        qf[kk] = __builtin_bit_cast(bf16x8, v);
+      }
+    }
+    const uint64_t rowbase = ((uint64_t)(b * H + h) * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
+    f32x4 ot[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, l = 0.f;
+    for (int j0 = 0; j0 < Lk; j0 += 32) {
+      // ---- S^T = K Q^T for keys j0 .. j0+31 ----
+      f32x4 st[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          const u32x4 kv = *(const u32x4*)(Ks + koff_k(j0 + nb * 16 + (lane & 15), kk * 4 + g));
+          st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv), qf[kk], st[nb], 0, 0, 0);
+        }
+      float s[8];
+      float tmax = -INFINITY;
+      const bool edge = j0 + 32 > Lk;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float v = st[nb][t] * sl2;
+          if (edge && j0 + nb * 16 + g * 4 + t >= Lk) v = -INFINITY;
+          s[nb * 4 + t] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);  // finite: every chunk holds >= 1 unmasked key
+      const float alpha = exp2f(m - mnew);
+      float p[8], psum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        p[k] = exp2f(s[k] - mnew);
+        psum += p[k];
+      }
+      psum += __shfl_xor(psum, 16, 64);
+      psum += __shfl_xor(psum, 32, 64);
+      l = l * alpha + psum;
+      m = mnew;
+      if (DROP) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            p[nb * 4 + t] *= drop_mul(key, rowbase + (uint64_t)(j0 + nb * 16 + g * 4 + t), a.thresh, a.dscale);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ot[i] *= alpha;
+      // ---- O^T += V^T P^T ----
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (bf16)p[j];
+        pb[4 + j] = (bf16)p[4 + j];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int colb = (i * 16 + 4 * pp) * 2;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vs + koff_v(j0 + g * 4 + q, colb)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vs + koff_v(j0 + 16 + g * 4 + q, colb)));
+        s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        ot[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pb, ot[i], 0, 0, 0);
+      }
+    }
+    if (qlive) {
+      const float inv = 1.0f / l;
+      bf16* O = (bf16*)a.o + b * a.o_batch + qi * a.o_row + h * D;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 o4 = {(bf16)(ot[i][0] * inv), (bf16)(ot[i][1] * inv), (bf16)(ot[i][2] * inv), (bf16)(ot[i][3] * inv)};
+        *(bf16x4*)(O + i * 16 + g * 4) = o4;
+      }
+      if (a.lse && g == 0) a.lse[(b * H + h) * Lq + qi] = (m + __log2f(l)) * 0.6931471805599453f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // bf16 MFMA backward, two kernels (launched dQ first: it also produces delta = rowsum(dO o O)).
 //   dQ kernel  (grid: query blocks): per 64-key tile  S^T = K Q^T, dP^T = V dO^T (A = K/V rows from
 //     LDS, B = Q/dO fragments in registers) -> dS^T -> dQ^T += K^T dS^T (A = K^T by transposed
@@ -705,10 +839,33 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
                        x->k_batch % 8 == 0 && x->v_row % 8 == 0 && x->v_batch % 8 == 0 && x->o_row % 4 == 0 &&
                        x->o_batch % 4 == 0 && ((uintptr_t)x->q | (uintptr_t)x->k | (uintptr_t)x->v) % 16 == 0 &&
                        ((uintptr_t)x->o % 8) == 0 && getenv("MIT_ATTN_SIMPLE") == nullptr;
+  static const int head_ok = getenv("MIT_ATTN_HEAD") ? atoi(getenv("MIT_ATTN_HEAD")) : 1;
   if (mfma_ok) {
     const long kb = 2 * ((Lk - 1) * x->k_row + D), vb = 2 * ((Lk - 1) * x->v_row + D);
     MIT_CHECK_ARG(kb < (1L << 31) && vb < (1L << 31), "mit_attention_fwd: K/V span >= 2 GiB");
-    hipLaunchKernelGGL(attn_fwd_mfma, grid, dim3(256), 0, s, H, Lq, Lk, a, (int)kb, (int)vb);
+    if (head_ok && !a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535) {
+      // head-resident K/V: one workgroup per (b, h), NW waves balanced over the 16-query tiles
+      const int lkp = (int)((Lk + 31) / 32 * 32);
+      const int nqt = (int)((Lq + 15) / 16);
+      const int rounds = (nqt + 15) / 16;
+      const int nw = (nqt + rounds - 1) / rounds;
+      const int lds = lkp * 256;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)attn_fwd_head<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  HK_MAX * 256);
+        (void)hipFuncSetAttribute((const void*)attn_fwd_head<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  HK_MAX * 256);
+        attr = true;
+      }
+      dim3 hg((unsigned)H, (unsigned)B);
+      if (a.dropout)
+        hipLaunchKernelGGL(attn_fwd_head<true>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
+      else
+        hipLaunchKernelGGL(attn_fwd_head<false>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
+    } else {
+      hipLaunchKernelGGL(attn_fwd_mfma, grid, dim3(256), 0, s, H, Lq, Lk, a, (int)kb, (int)vb);
+    }
   } else if (dtype == MIT_BF16)
     hipLaunchKernelGGL(attn_fwd_simple<bf16>, grid, dim3(64), 0, s, H, Lq, Lk, a);
   else

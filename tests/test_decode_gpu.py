@@ -133,14 +133,20 @@ def test_generate_batch_matches_full_recompute(name):
         assert batch[b] == single, (b, batch[b], single)
 
 
-def test_generate_batch_bf16_agrees_with_fp32():
-    """bf16 decode tracks the fp32 one (same weights): first tokens identical, >= 80 % overall."""
-    m32, meta, _ = _trained("tiny_vit_patches", torch.float32)
-    m16, _, _ = _trained("tiny_vit_patches", torch.bfloat16)
+def test_generate_batch_bf16_consistent_with_full_forward():
+    """bf16: every token the KV-cached decode picked is the argmax of the model's full (non-cached)
+    forward over the same prefix, except where that forward's top-1/top-2 logit margin is a bf16
+    near-tie (< 3e-2) — the decode path computes the reference's recompute up to rounding."""
+    m, meta, _ = _trained("tiny_vit_patches", torch.bfloat16)
     img = FX.inputs(meta, 0)[0]
-    a = m32.generate_batch(img, 2, 3, max_len=16)
-    b = m16.generate_batch(img, 2, 3, max_len=16)
-    same = sum(x == y for ra, rb in zip(a, b) for x, y in zip(ra, rb))
-    total = sum(min(len(ra), len(rb)) for ra, rb in zip(a, b))
-    assert all(ra[1] == rb[1] for ra, rb in zip(a, b))
-    assert same >= 0.8 * total
+    imgs = torch.cat([img, img.flip(-1)], 0)
+    never = 10 ** 6  # run every caption to max_len
+    ids = m.generate_batch(imgs, 2, never, max_len=20)
+    seq = torch.tensor(ids)
+    with torch.no_grad():
+        logits = m(imgs.cuda(), seq[:, :-1].cuda()).float().cpu()
+    top2 = logits.topk(2, -1).values
+    margin = top2[..., 0] - top2[..., 1]
+    agree = logits.argmax(-1) == seq[:, 1:]
+    assert bool((agree | (margin < 3e-2)).all()), (agree, margin)
+    assert agree.float().mean().item() > 0.9

@@ -168,13 +168,15 @@ def _attn_ref(q, k, v, causal, kpm, scale, drop=None):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("kind", ["self_causal_pad", "cross", "bidir", "cross_s1", "self_drop", "self_long",
-                                  "cross577"])
+                                  "cross577", "cross_drop", "bidir577"])
 def test_attention_fwd_bwd(dtype, kind):
     B, H, D = 3, 4, 64
     if kind == "self_causal_pad" or kind == "self_drop":
         Lq = Lk = 63
-    elif kind == "cross":
+    elif kind in ("cross", "cross_drop"):
         Lq, Lk = 63, 197
+    elif kind == "bidir577":
+        Lq = Lk = 577  # CLIP-L/14@336 encoder MHSA: 37 query tiles over 3 rounds of waves
     elif kind == "cross_s1":
         Lq, Lk = 31, 1
     elif kind == "self_long":
@@ -184,7 +186,7 @@ def test_attention_fwd_bwd(dtype, kind):
     else:
         Lq = Lk = 197
     causal = kind.startswith("self")
-    drop_p = 0.1 if kind == "self_drop" else 0.0
+    drop_p = 0.1 if kind in ("self_drop", "cross_drop") else 0.0
     q = torch.randn(B, Lq, H * D, device=dev()).to(dtype)
     kv = torch.randn(B, Lk, 2 * H * D, device=dev()).to(dtype)
     k, v = kv[..., :H * D], kv[..., H * D:]
