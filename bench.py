@@ -265,6 +265,8 @@ def main():
                          "weight-gradient stream run beside the main stream (measured faster than the graph, whose "
                          "parallel branches ROCm 7 does not overlap)")
     ap.add_argument("--no-graph", action="store_true", help="(default; kept for older scripts)")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="run the frozen encoder inside each step instead of one step ahead on a second stream")
     ap.add_argument("--workload", default="train", choices=["train", "decode"],
                     help="train: the BASELINE metric (default). decode: configs[4], batched greedy captioning "
                          "(KV cache, hipGraph-replayed token step)")
@@ -285,8 +287,12 @@ def main():
     model.train()
     images, di, tg = synthetic_batch(args.batch, args.seq_len, args.vocab, dev, 1000 + rank)
 
+    prefetch = not args.no_prefetch
+
     def eager_step():
-        return model.train_step(images, di, tg, dist=dp)
+        # the frozen encoder's forward for the next batch runs on a second stream beside this
+        # step's decoder work (model.prefetch_encoder); one encoder forward per step either way
+        return model.train_step(images, di, tg, dist=dp, next_images=images if prefetch else None)
 
     use_graph = world == 1 and args.graph and not args.no_graph
     if use_graph:

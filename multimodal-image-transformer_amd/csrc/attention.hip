@@ -446,17 +446,18 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
 // ------------------------------------------------------------------------------------------------
 // bf16 MFMA forward, head-resident K/V (no causal / PAD mask: the encoder MHSA and the decoder
 // cross-attention). One workgroup per (b, h) stages the WHOLE K and V of the head in LDS once
-// (Lk rounded up to 32 rows, <= 640 rows = 160 KiB; rows past Lk read as zero and are masked),
+// (Lk rounded up to 64 rows, <= 640 rows = 160 KiB; rows past Lk read as zero and are masked),
 // then NW waves sweep 16-query tiles (ceil(Lq/16) tiles, so L = 197 wastes 5 % instead of the 30 %
 // of 64-query blocks) against 32-key chunks with no barrier, no global load and no LDS write inside
-// the key loop. Per chunk and wave: S^T = K Q^T (4 MFMAs) -> online softmax on 8 in-lane scores ->
-// O^T += V^T P^T (4 MFMAs, P straight from the accumulators, same permutation as attn_fwd_mfma).
+// the key loop. Per 64-key chunk and wave: S^T = K Q^T (8 MFMAs) -> online softmax on 16 in-lane
+// scores (scale folded into the exp2 FMA) -> O^T += V^T P^T (8 MFMAs, P straight from the
+// accumulators, same key permutation as attn_fwd_mfma per 32-key half).
 // Dropout (decoder cross-attention in training) is a template flag.
 // ------------------------------------------------------------------------------------------------
 constexpr int HK_MAX = 640;  // keys per head the LDS can hold (K + V = 256 B per key)
 
 template <bool DROP>
-__global__ __launch_bounds__(1024) void attn_fwd_head(long H, long Lq, long Lk, AttnK a, int kbytes, int vbytes,
+__global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) void attn_fwd_head(long H, long Lq, long Lk, AttnK a, int kbytes, int vbytes,
                                                       int lkp) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* Ks = lds;
@@ -484,6 +485,17 @@ __global__ __launch_bounds__(1024) void attn_fwd_head(long H, long Lq, long Lk, 
   const uint64_t key = DROP ? site_key(a.seed, a.site) : 0ull;
   const int nqt = (int)((Lq + 15) / 16);
   const int q = (lane & 15) >> 2, pp = lane & 3;
+  // LDS byte offsets at key chunk 0; the swizzles only see row bits below 5, so chunk j0 (a
+  // multiple of 32) just adds j0 * 128
+  const int kofs = koff_k(lane & 15, g);           // + nb*2048 (16 rows), kk: chunk c ^ 4
+  const int kofs1 = koff_k(lane & 15, 4 + g);
+  int vofs[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int colb = (i * 16 + 4 * pp) * 2;
+    vofs[i][0] = koff_v(g * 4 + q, colb);
+    vofs[i][1] = koff_v(16 + g * 4 + q, colb);
+  }
   for (int qt = w; qt < nqt; qt += nw) {
     const long qi = (long)qt * 16 + (lane & 15);
     const bool qlive = qi < Lq;
@@ -502,36 +514,51 @@ __global__ __launch_bounds__(1024) void attn_fwd_head(long H, long Lq, long Lk, 
 #pragma unroll
     for (int i = 0; i < 4; ++i) ot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, l = 0.f;
-    for (int j0 = 0; j0 < Lk; j0 += 32) {
-      // ---- S^T = K Q^T for keys j0 .. j0+31 ----
-      f32x4 st[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const char* Kc = Ks;
+    const char* Vc = Vs;
+    for (int j0 = 0; j0 < Lk; j0 += 64, Kc += 64 * 128, Vc += 64 * 128) {
+      // ---- S^T = K Q^T for keys j0 .. j0+63 (4 key tiles of 16) ----
+      f32x4 st[4];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int nb = 0; nb < 4; ++nb) {
+        const u32x4 k0 = *(const u32x4*)(Kc + nb * 2048 + kofs);
+        const u32x4 k1 = *(const u32x4*)(Kc + nb * 2048 + kofs1);
+        st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k0), qf[0],
+                                                          f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k1), qf[1], st[nb], 0, 0, 0);
+      }
+      // V^T fragments (2 x 32-key halves x 4 d-tiles): issued before the softmax to hide latency
+      s16x8 vv[2][4];
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-          const u32x4 kv = *(const u32x4*)(Ks + koff_k(j0 + nb * 16 + (lane & 15), kk * 4 + g));
-          st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv), qf[kk], st[nb], 0, 0, 0);
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + hh * 4096 + vofs[i][0]));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + hh * 4096 + vofs[i][1]));
+          vv[hh][i] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
-      float s[8];
-      float tmax = -INFINITY;
-      const bool edge = j0 + 32 > Lk;
+      // scores stay unscaled: max commutes with the positive scale, which folds into the exp2 FMA
+      float s[16];
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
+      for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          float v = st[nb][t] * sl2;
-          if (edge && j0 + nb * 16 + g * 4 + t >= Lk) v = -INFINITY;
-          s[nb * 4 + t] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(m, tmax);  // finite: every chunk holds >= 1 unmasked key
-      const float alpha = exp2f(m - mnew);
-      float p[8], psum = 0.f;
+        for (int t = 0; t < 4; ++t) s[nb * 4 + t] = st[nb][t];
+      if (j0 + 64 > Lk) {  // ragged last chunk (wave-uniform)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        p[k] = exp2f(s[k] - mnew);
+        for (int k = 0; k < 16; ++k)
+          if (j0 + (k >> 2) * 16 + g * 4 + (k & 3) >= Lk) s[k] = -INFINITY;
+      }
+      float tmax = s[0];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) tmax = __builtin_fmaxf(tmax, s[k]);
+      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = __builtin_fmaxf(m, tmax * sl2);  // finite: >= 1 unmasked key per chunk
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      float p[16], psum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        p[k] = __builtin_amdgcn_exp2f(fmaf(s[k], sl2, -mnew));
         psum += p[k];
       }
       psum += __shfl_xor(psum, 16, 64);
@@ -540,27 +567,22 @@ __global__ __launch_bounds__(1024) void attn_fwd_head(long H, long Lq, long Lk, 
       m = mnew;
       if (DROP) {
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+        for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             p[nb * 4 + t] *= drop_mul(key, rowbase + (uint64_t)(j0 + nb * 16 + g * 4 + t), a.thresh, a.dscale);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) ot[i] *= alpha;
-      // ---- O^T += V^T P^T ----
-      bf16x8 pb;
+      // ---- O^T += V^T P^T, two 32-key halves ----
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[j] = (bf16)p[j];
-        pb[4 + j] = (bf16)p[4 + j];
-      }
+      for (int hh = 0; hh < 2; ++hh) {
+        bf16x8 pb;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int colb = (i * 16 + 4 * pp) * 2;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vs + koff_v(j0 + g * 4 + q, colb)));
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vs + koff_v(j0 + 16 + g * 4 + q, colb)));
-        s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        ot[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pb, ot[i], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) pb[j] = (bf16)p[hh * 8 + j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ot[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv[hh][i]), pb, ot[i], 0, 0, 0);
       }
     }
     if (qlive) {
@@ -845,9 +867,12 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
     MIT_CHECK_ARG(kb < (1L << 31) && vb < (1L << 31), "mit_attention_fwd: K/V span >= 2 GiB");
     if (head_ok && !a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535) {
       // head-resident K/V: one workgroup per (b, h), NW waves balanced over the 16-query tiles
-      const int lkp = (int)((Lk + 31) / 32 * 32);
+      const int lkp = (int)((Lk + 63) / 64 * 64);
       const int nqt = (int)((Lq + 15) / 16);
-      const int rounds = (nqt + 15) / 16;
+      // <= 8 waves whenever two heads fit the LDS, so a CU holds two workgroups and one stages its
+      // K/V while the other computes; the dropout instance is built for <= 512 threads
+      const int maxw = (a.dropout || 2 * lkp * 256 <= 160 * 1024) ? 8 : 16;
+      const int rounds = (nqt + maxw - 1) / maxw;
       const int nw = (nqt + rounds - 1) / rounds;
       const int lds = lkp * 256;
       static bool attr = false;

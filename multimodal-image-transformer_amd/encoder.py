@@ -191,10 +191,13 @@ class VisionEncoder:
         return self.load_hf_state_dict(sd)
 
     # --- forward -----------------------------------------------------------------------------
-    def _workspace(self, B):
-        if B not in self._ws:
+    def _workspace(self, B, slot=0):
+        """Activation arena per (batch, slot): slot 1 is a second arena so a forward for the NEXT
+        batch can run on another stream while this batch's output is still being read."""
+        key = (B, slot)
+        if key not in self._ws:
             R, E, dt, dev = B * self.N, self.E, self.dtype, self.device
-            self._ws[B] = dict(
+            self._ws[key] = dict(
                 cols=torch.empty(B * self.np, self.kpad, dtype=dt, device=dev),
                 pt=torch.empty(B * self.np, E, dtype=dt, device=dev),
                 h=torch.empty(R, E, dtype=dt, device=dev),
@@ -204,9 +207,9 @@ class VisionEncoder:
                 m=torch.empty(R, self.mlp, dtype=dt, device=dev),
                 out=torch.empty(R, E, dtype=dt, device=dev),
             )
-        return self._ws[B]
+        return self._ws[key]
 
-    def forward(self, images: torch.Tensor, rows: str = "all") -> torch.Tensor:
+    def forward(self, images: torch.Tensor, rows: str = "all", slot: int = 0) -> torch.Tensor:
         """images f32 [B,3,H,W] (already normalised) -> last_hidden_state in the compute dtype.
         rows="all": [B, N, E] ; rows="cls": only the CLS rows are finalised, returned as the
         strided view [B, E] of the [B, N, E] buffer (row stride N*E)."""
@@ -214,7 +217,7 @@ class VisionEncoder:
         if tuple(images.shape[1:]) != (3, self.image, self.image):
             raise ValueError(f"expected images [B,3,{self.image},{self.image}], got {tuple(images.shape)}")
         images = images.contiguous().float()
-        ws, w, E, N, H = self._workspace(B), self.w, self.E, self.N, self.H
+        ws, w, E, N, H = self._workspace(B, slot), self.w, self.E, self.N, self.H
         R = B * N
         native.im2col(images, ws["cols"], self.patch, self.kpad)
         native.linear(ws["cols"], w["patch.w"], ws["pt"], bias=w["patch.b"])

@@ -115,6 +115,9 @@ class ImageToTextModel:
         # dropout RNG state: a device counter (graph-replay safe), distinct per DP rank
         self.seed_t = torch.tensor([seed * 1000003], dtype=torch.int64, device=self.device)
         self._mem: Dict[tuple, torch.Tensor] = {}
+        self._enc_stream = None
+        self._enc_slot = 0
+        self._prefetched = None
 
     # --- nn.Module-like surface ----------------------------------------------------------------
     def train(self, mode: bool = True):
@@ -142,17 +145,44 @@ class ImageToTextModel:
         self.seed_t.fill_(seed * 1000003 + rank * 7919 * 65537)
 
     # --- memory (encoder -> projection) ----------------------------------------------------------
+    def _encoder_rows(self, images: torch.Tensor, slot: int = 0):
+        """Frozen encoder -> (enc_rows, enc_ld, S): the rows that feed the projection."""
+        B = images.shape[0]
+        N, E = self.encoder.N, self.encoder.E
+        if self.memory_mode == "cls":
+            enc = self.encoder.forward(images, rows="cls", slot=slot)  # [B, E] view, row stride N*E
+            return enc, N * E, 1
+        enc = self.encoder.forward(images, rows="all", slot=slot)  # [B, N, E]
+        return enc.reshape(B * N, E), E, N
+
+    def prefetch_encoder(self, images: torch.Tensor):
+        """Start the frozen encoder's forward for the NEXT batch on a second stream; the next
+        train_step(images) consumes it instead of recomputing. The encoder has no trainable state, so
+        its output does not depend on the step in between: the result is identical, and its GEMMs
+        fill the CUs the decoder's small kernels leave idle. Double-buffered arenas (slot 0/1)."""
+        if self._enc_stream is None:
+            self._enc_stream = torch.cuda.Stream(device=self.device)
+        slot = 1 - self._enc_slot
+        images = images.to(self.device, non_blocking=True)
+        main = torch.cuda.current_stream(self.device)
+        self._enc_stream.wait_stream(main)  # the arena's previous reader (two steps back) is done
+        with torch.cuda.stream(self._enc_stream):
+            out = self._encoder_rows(images, slot)
+        ev = torch.cuda.Event()
+        ev.record(self._enc_stream)
+        self._prefetched = (images, slot, out, ev)
+
     def _encode_memory(self, images: torch.Tensor):
         """Returns (mem_rows, mem_ld, S, enc_rows, enc_ld): memory [B*S rows of d] and the
         encoder features that feed the projection (for its weight gradient)."""
         B = images.shape[0]
-        N, E, d = self.encoder.N, self.encoder.E, self.decoder_embed_dim
-        if self.memory_mode == "cls":
-            enc = self.encoder.forward(images, rows="cls")  # [B, E] view, row stride N*E
-            S, enc_rows, enc_ld = 1, enc, N * E
+        E, d = self.encoder.E, self.decoder_embed_dim
+        pf, self._prefetched = self._prefetched, None
+        if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
+            _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
+            torch.cuda.current_stream(self.device).wait_event(ev)
         else:
-            enc = self.encoder.forward(images, rows="all")  # [B, N, E]
-            S, enc_rows, enc_ld = N, enc.reshape(B * N, E), E
+            enc_rows, enc_ld, S = self._encoder_rows(images, self._enc_slot)
         if not self.has_projection:
             return enc_rows, enc_ld, S, enc_rows, enc_ld
         key = (B, S)
@@ -181,14 +211,18 @@ class ImageToTextModel:
 
     # --- fused train step (train.py:75-93) -----------------------------------------------------
     def train_step(self, images: torch.Tensor, decoder_input_tokens: torch.Tensor, target_tokens: torch.Tensor,
-                   dist=None) -> torch.Tensor:
+                   dist=None, next_images: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward + CE(ignore PAD, mean over the GLOBAL non-PAD count) + backward into the flat
-        gradient buffer. Returns the loss as a device scalar [1] (no host sync)."""
+        gradient buffer. Returns the loss as a device scalar [1] (no host sync).
+        next_images: the next batch's images, whose (frozen) encoder forward then runs on a second
+        stream beside this step's decoder work (prefetch_encoder); results are unchanged."""
         images = images.to(self.device, non_blocking=True)
         tokens = decoder_input_tokens.to(self.device, torch.int64, non_blocking=True).contiguous()
         targets = target_tokens.to(self.device, torch.int64, non_blocking=True).contiguous()
         B, T = tokens.shape
         mem, mem_ld, S, enc_rows, enc_ld = self._encode_memory(images)
+        if next_images is not None:
+            self.prefetch_encoder(next_images)
         dec = self.decoder
         A = dec.acts(B, T, S, True)
         native.step_inc(self.seed_t)

@@ -236,3 +236,32 @@ def test_graphed_step_matches_eager():
     (l0, p0), (l1, p1) = res
     assert all(abs(a - b) < 1e-3 for a, b in zip(l0, l1)), (l0, l1)
     torch.testing.assert_close(p1, p0, rtol=0, atol=1e-4)
+
+
+def test_encoder_prefetch_matches_inline():
+    """train_step(..., next_images=...) runs the frozen encoder of the next batch one step ahead on
+    a second stream (double-buffered arenas); losses and parameters equal the inline schedule,
+    including when the batch changes between steps."""
+    import optim
+    meta, T = FX.load("tiny_vit_patches")
+    batches = [[t.cuda() for t in FX.inputs(meta, s)] for s in range(3)]
+    res = []
+    for prefetch in (False, True):
+        m, _ = build_model(meta, torch.float32, dropout=0.1)
+        m.train()
+        opt = optim.AdamW(m.store, lr=1e-3)
+        losses = []
+        for s in range(4):
+            imgs, di, tg = batches[s % 3]
+            nxt = batches[(s + 1) % 3][0] if prefetch else None
+            losses.append(m.train_step(imgs, di, tg, next_images=nxt).item())
+            opt.step(5.0)
+        res.append((losses, m.store.master.clone()))
+    (l0, p0), (l1, p1) = res
+    assert all(abs(a - b) < 1e-5 for a, b in zip(l0, l1)), (l0, l1)
+    # the embedding gradient is a float atomic scatter-add (summation order varies run to run);
+    # AdamW's g/sqrt(v) turns last-ulp differences of near-zero gradients into update-sized ones
+    # (<= 2 lr) on a few elements — the same spread two inline runs show
+    diff = (p1 - p0).abs()
+    assert diff.max().item() <= 2.5e-3
+    assert (diff > 1e-5).float().mean().item() < 5e-3

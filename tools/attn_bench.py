@@ -1,0 +1,44 @@
+"""Micro-benchmark of mit_attention_fwd on the train step's shapes (bf16, random operands):
+encoder MHSA (ViT-B/16: L=197, 12 heads; CLIP-L/14@336: L=577, 16 heads) and the decoder
+cross-attention (63 queries over 197 patches, 8 heads). Prints us and TFLOP/s (4*Lq*Lk*64/head)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-image-transformer_amd"))
+import torch  # noqa: E402
+
+import native  # noqa: E402
+
+SHAPES = [("enc vit-b16", 64, 12, 197, 197), ("dec cross", 64, 8, 63, 197), ("enc clip-l336", 16, 16, 577, 577)]
+
+
+def run(iters=20):
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(0)
+    for name, B, H, Lq, Lk in SHAPES:
+        E = H * 64
+        qkv = torch.randn(B, max(Lq, Lk), 3 * E, generator=g).to(dev, torch.bfloat16)
+        o = torch.empty(B, Lq, E, device=dev, dtype=torch.bfloat16)
+        lse = torch.empty(B * H * Lq, device=dev)
+        T = max(Lq, Lk)
+        a = native.attn_args(qkv, 3 * E, T * 3 * E, qkv[..., E:], 3 * E, T * 3 * E, qkv[..., 2 * E:], 3 * E, T * 3 * E,
+                             o, E, Lq * E, lse=lse, scale=0.125)
+        for _ in range(3):
+            native.attention_fwd(native.BF16, B, H, Lq, Lk, a)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            native.attention_fwd(native.BF16, B, H, Lq, Lk, a)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / iters * 1e-3
+        fl = 4.0 * B * H * Lq * Lk * 64
+        print(f"{name:14s} B={B:3d} H={H:2d} Lq={Lq:4d} Lk={Lk:4d}  {t * 1e6:8.1f} us  {fl / t / 1e12:7.1f} TFLOP/s",
+              flush=True)
+
+
+if __name__ == "__main__":
+    native.load_library()
+    run()
