@@ -36,9 +36,25 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
     model.train()
     total = torch.zeros(1, dtype=torch.float32, device=model.device)
     n = 0
-    for i, batch in enumerate(dataloader):
+
+    def staged(it):
+        # images go to the device once, so the next step can consume the encoder output that
+        # model.prefetch_encoder computed for this very tensor one step earlier
+        for b in it:
+            b = dict(b)
+            b["images"] = b["images"].to(model.device, non_blocking=True)
+            yield b
+
+    it = staged(dataloader)
+    batch = next(it, None)
+    i = -1
+    while batch is not None:
+        i += 1
+        nxt = next(it, None)
         optimizer.zero_grad()
-        loss = model.train_step(batch["images"], batch["decoder_input_tokens"], batch["target_tokens"], dist=dist)
+        # the frozen encoder of the NEXT batch runs on a second stream during this step
+        loss = model.train_step(batch["images"], batch["decoder_input_tokens"], batch["target_tokens"], dist=dist,
+                                next_images=nxt["images"] if nxt is not None else None)
         optimizer.step(grad_clip_value if grad_clip_value > 0 else 0.0)
         if scheduler:
             scheduler.step()
@@ -50,6 +66,7 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
             if wandb_run:
                 wandb_run.log({"train_batch_loss": lv, "learning_rate": _lr_of(optimizer),
                                "global_step": epoch * max(1, len(dataloader)) + i + 1})
+        batch = nxt
     return (total / max(n, 1)).item()
 
 
@@ -90,6 +107,13 @@ class LinearWarmup:
     def get_last_lr(self):
         return [_lr_of(self.opt)]
 
+    def state_dict(self):
+        return {"step_n": self.step_n, "base": self.base, "w": self.w, "t": self.t}
+
+    def load_state_dict(self, sd):
+        self.step_n, self.base, self.w, self.t = sd["step_n"], sd["base"], sd["w"], sd["t"]
+        self._apply()
+
 
 def synthetic_loader(n_batches, B, seq_len, vocab, image, seed=0):
     g = torch.Generator().manual_seed(seed)
@@ -102,16 +126,46 @@ def synthetic_loader(n_batches, B, seq_len, vocab, image, seed=0):
     return out
 
 
-def save_checkpoint(model, optimizer, epoch, val_loss, path_prefix):
-    """train.py:412-442: a .pt dict {epoch, model_state_dict, optimizer_state_dict, best_val_loss}
-    and a .safetensors of model.state_dict() (reference key names)."""
+def save_checkpoint(model, optimizer, epoch, val_loss, path_prefix, scheduler=None):
+    """train.py:412-442: a .pt dict {epoch, model_state_dict, optimizer_state_dict,
+    scheduler_state_dict, best_val_loss} and a .safetensors of model.state_dict() (reference key
+    names)."""
     from safetensors.torch import save_file
     name = f"{path_prefix}_{config.ENCODER_MODEL_NAME.replace('/', '_')}_epoch_{epoch + 1}_val_loss_{val_loss:.4f}"
     sd = {k: v.detach().cpu().contiguous() for k, v in model.state_dict().items()}
     torch.save({"epoch": epoch, "model_state_dict": sd, "optimizer_state_dict": optimizer.state_dict(),
+                "scheduler_state_dict": scheduler.state_dict() if scheduler is not None else None,
                 "best_val_loss": val_loss}, name + ".pt")
     save_file(sd, name + ".safetensors")
     return name
+
+
+def load_checkpoint(model, optimizer, scheduler, path):
+    """train.py:343-375: resume from a .pt checkpoint written by save_checkpoint -> (start_epoch,
+    best_val_loss). A missing or unreadable file means training from scratch (0, inf), as the
+    reference does. Loaded with torch.load(weights_only=True): the dict holds only tensors and
+    plain containers, so nothing in the file is executed (the reference uses weights_only=False).
+    A .safetensors path (inference.py:66-67) restores the model weights only."""
+    if not path or not os.path.exists(path):
+        if path:
+            print(f"Warning: checkpoint '{path}' does not exist. Starting training from scratch.")
+        return 0, math.inf
+    try:
+        if path.endswith(".safetensors"):
+            from safetensors.torch import load_file
+            model.load_state_dict(load_file(path))
+            return 0, math.inf
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        model.load_state_dict(ck["model_state_dict"])
+        optimizer.load_state_dict(ck["optimizer_state_dict"])
+        if scheduler is not None and ck.get("scheduler_state_dict"):
+            scheduler.load_state_dict(ck["scheduler_state_dict"])
+        start = ck["epoch"] + 1
+        print(f"Successfully resumed training. Starting from epoch {start}.")
+        return start, ck.get("best_val_loss", math.inf)
+    except Exception as e:  # noqa: BLE001 — the reference falls back to scratch on any load error
+        print(f"Error loading checkpoint: {e}. Starting training from scratch.")
+        return 0, math.inf
 
 
 def main(argv=None):
@@ -121,6 +175,8 @@ def main(argv=None):
     ap.add_argument("--batch-size", type=int, default=config.BATCH_SIZE)
     ap.add_argument("--seq-len", type=int, default=64)
     ap.add_argument("--out", default=None, help="checkpoint prefix (optional)")
+    ap.add_argument("--resume", default=getattr(config, "RESUME_CHECKPOINT_PATH", None),
+                    help="resume from a .pt checkpoint (train.py:343-375)")
     args = ap.parse_args(argv)
     torch.manual_seed(config.RANDOM_SEED)
     model = ImageToTextModel(config.VOCAB_SIZE, config.DECODER_EMBED_DIM, config.DECODER_HEADS, config.DECODER_LAYERS,
@@ -132,8 +188,8 @@ def main(argv=None):
         sched = LinearWarmup(opt, config.WARMUP_STEPS, args.batches * args.epochs)
     train = synthetic_loader(args.batches, args.batch_size, args.seq_len, config.VOCAB_SIZE, model.encoder.image, 1)
     val = synthetic_loader(2, args.batch_size, args.seq_len, config.VOCAB_SIZE, model.encoder.image, 2)
-    best = math.inf
-    for epoch in range(args.epochs):
+    start, best = load_checkpoint(model, opt, sched, args.resume)
+    for epoch in range(start, args.epochs):
         t0 = time.time()
         tl = train_one_epoch(model, train, opt, None, "cuda", config.GRAD_CLIP_VALUE, sched, epoch, config.LOG_INTERVAL,
                              None)
@@ -141,7 +197,7 @@ def main(argv=None):
         print(f"epoch {epoch + 1}: train {tl:.4f} val {vl:.4f} ({time.time() - t0:.1f}s)", flush=True)
         if vl < best and args.out:
             best = vl
-            print("saved", save_checkpoint(model, opt, epoch, vl, args.out))
+            print("saved", save_checkpoint(model, opt, epoch, vl, args.out, sched))
 
 
 if __name__ == "__main__":

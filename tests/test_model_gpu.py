@@ -265,3 +265,50 @@ def test_encoder_prefetch_matches_inline():
     diff = (p1 - p0).abs()
     assert diff.max().item() <= 2.5e-3
     assert (diff > 1e-5).float().mean().item() < 5e-3
+
+
+def test_checkpoint_save_resume_roundtrip(tmp_path):
+    """train.save_checkpoint -> train.load_checkpoint (train.py:343-375, 412-442): a resumed model
+    continues EXACTLY where the original left off (weights, AdamW moments, step count, scheduler);
+    the .safetensors restores weights only (inference.py:66-67)."""
+    import optim
+    import train as TR
+    meta, _ = FX.load("tiny_vit_patches")
+    batches = [[t.cuda() for t in FX.inputs(meta, s)] for s in range(3)]
+
+    def fresh():
+        m, _ = build_model(meta, torch.float32)
+        m.train()
+        opt = optim.AdamW(m.store, lr=1e-3)
+        sch = TR.LinearWarmup(opt, 2, 10)
+        return m, opt, sch
+
+    def step(m, opt, sch, b):
+        loss = m.train_step(*b)
+        opt.step(5.0)
+        sch.step()
+        return loss.item()
+
+    m, opt, sch = fresh()
+    for b in batches[:2]:
+        step(m, opt, sch, b)
+    name = TR.save_checkpoint(m, opt, 0, 1.2345, str(tmp_path / "ck"), sch)
+    ref_next = step(m, opt, sch, batches[2])
+    ref_params = m.store.master.clone()
+
+    m2, opt2, sch2 = fresh()
+    start, best = TR.load_checkpoint(m2, opt2, sch2, name + ".pt")
+    assert start == 1 and abs(best - 1.2345) < 1e-9
+    assert step(m2, opt2, sch2, batches[2]) == ref_next
+    torch.testing.assert_close(m2.store.master, ref_params, rtol=0, atol=0)
+
+    m3, opt3, sch3 = fresh()
+    assert TR.load_checkpoint(m3, opt3, sch3, name + ".safetensors") == (0, float("inf"))
+    m3.eval()
+    m2b, _, _ = fresh()
+    TR.load_checkpoint(m2b, optim.AdamW(m2b.store, lr=1e-3), None, name + ".pt")
+    m2b.eval()
+    imgs, di, _ = batches[0]
+    with torch.no_grad():
+        torch.testing.assert_close(m3(imgs, di), m2b(imgs, di), rtol=0, atol=0)
+    assert TR.load_checkpoint(m3, opt3, sch3, str(tmp_path / "missing.pt")) == (0, float("inf"))
