@@ -53,8 +53,13 @@ int mit_abi_version(void);
  *   out_f32: write f32 (accumulate: C += value), else the operand dtype.
  *   rowsum (optional, f32 [M]): rowsum[m] = sum_k A(m,k) — the bias gradient when A = dY^T in a
  *     weight-gradient GEMM, fused in (no separate column-sum pass over dY).
- *   workspace: scratch for split-K (plain-epilogue GEMMs with few output tiles and a long K, i.e.
- *     weight gradients); size from mit_gemm_workspace_bytes(M, N, K). NULL / too small -> no split.
+ *   workspace: split-K scratch, size from mit_gemm_workspace_bytes(M, N, K); NULL / too small -> no
+ *     split. Zero-fill it ONCE before first use: its first 4 KiB hold per-tile counters that every
+ *     launch leaves at zero. One workspace per stream (launches sharing one must be ordered). Two
+ *     split forms: plain-epilogue GEMMs with few output tiles and a long K (weight gradients) write
+ *     fp32 partials and a second launch reduces them; with mit_gemm_set_fused_split(1), grids of
+ *     <= 128 output tiles with any other epilogue but rowsum combine in-launch: the last K slice of
+ *     a tile to finish sums the slabs in slice order and runs the epilogue (deterministic).
  * bf16 requirements: lda, ldb and the contiguous extent of each operand multiples of 8; A, B 16-B aligned. */
 typedef struct {
   int dtype, a_layout, b_layout;
@@ -88,6 +93,9 @@ long mit_gemm_workspace_bytes(long M, long N, long K);
  * 1 = 128x128 kernel only, 2 = 256x256 kernel wherever split-K is not planned. Results are
  * identical up to fp32 summation order; a tuning / test knob, not a numerics switch. */
 int mit_gemm_set_variant(int variant);
+/* In-launch split-K combine (see workspace above): 0 = off (default; env MIT_GEMM_FUSED_SPLIT=1
+ * seeds it on), 1 = on. A scheduling knob: results equal up to fp32 summation order. */
+int mit_gemm_set_fused_split(int on);
 /* The launch mit_gemm would make for these args (no launch): returns the output tile edge of the
  * kernel (256 or 128 for bf16, 64 for the f32 kernel, 0 for an empty problem) and stores the
  * split-K factor in *ksplit (may be NULL). For profiling tools that attribute kernel time. */

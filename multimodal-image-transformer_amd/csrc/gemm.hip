@@ -147,7 +147,10 @@ __device__ __forceinline__ void epi_row8(const Epi& e, void* C, long ldc, long N
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE_BYTES = BM * BK * 2;          // 16 KiB per operand per stage
 constexpr int CST = BN + 4;                      // fp32 C-tile row stride in LDS (floats)
-constexpr int SMEM_BYTES = (4 * TILE_BYTES > BM * CST * 4) ? 4 * TILE_BYTES : BM * CST * 4;
+// + 16 B past the fp32 C stage: the split-K combine's "last slice" flag
+constexpr int smem_bytes(int nst) {
+  return (2 * nst * TILE_BYTES > BM * CST * 4 + 16) ? 2 * nst * TILE_BYTES : BM * CST * 4 + 16;
+}
 constexpr uint32_t OOB = 0x80000000u;            // buffer offset past any num_records -> loads 0
 
 // byte offset of 16-B chunk c (0..7) of row r in a K-contig [128][64] bf16 tile
@@ -225,11 +228,23 @@ __device__ __forceinline__ float frag_rowsum(bf16x8 a, float r) {
 // ------------------------------------------------------------------------------------------------
 // bf16 MFMA kernel, 128x128 block tile
 // ------------------------------------------------------------------------------------------------
-template <int ALAY, int BLAY, int ACT, bool DROP>
+template <int NST>
+__device__ __forceinline__ void wait_tiles(int younger) {  // this wave's DMAs of all but `younger` tiles landed
+  if (NST > 3 && younger >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (NST > 2 && younger == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (younger >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// NST = LDS stages (K-tiles resident at once). Launched with 2 (64 KiB: two blocks per CU). Four
+// stages (three tiles in flight) on the 1-block-per-CU decoder grids measured no faster (within
+// 2 %, tools/gemm_bench.py): those blocks are bound by per-iteration latency, not DMA depth.
+template <int ALAY, int BLAY, int ACT, bool DROP, int NST>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                         long M, long N, long K, long lda, long ldb, long ldc,
                                                         int a_bytes, int b_bytes, Epi e, int ksplit, long kchunk,
-                                                        float* __restrict__ ws, float* __restrict__ rowsum) {
+                                                        float* __restrict__ ws, float* __restrict__ rowsum,
+                                                        int* __restrict__ tile_cnt, long ws_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -237,9 +252,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   const int nbn = (int)((N + BN - 1) / BN), nbm = (int)((M + BM - 1) / BM);
   const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
   int bid = xcd_remap(blockIdx.x, nwg);
-  // split-K: slice `split` covers k in [kb, ke)
-  const int split = bid / ntiles;
-  bid -= split * ntiles;
+  // split-K: slice `split` covers k in [kb, ke); a tile's slices are neighbours in the remapped
+  // order, i.e. on one XCD (the in-launch combine below reads same-XCD slabs fastest)
+  const int split = bid % ksplit;
+  bid /= ksplit;
   const long kb = (long)split * kchunk, ke = min(K, kb + kchunk);
   // groups of 8 M-blocks walk the N-blocks together (B panel reuse in L2)
   const int GROUP = 8;
@@ -287,19 +303,23 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     }
   };
 
-  // LDS-DMA, two stages: the next tile's DMA is in flight while this tile computes; counted vmcnt
-  // + raw barriers (a __syncthreads() would drain the in-flight DMA with vmcnt(0), guide §5)
-  glds_tile<ALAY>(ra, AS(0), lda, M, ke, m0, kb, wid, lane);
-  glds_tile<BLAY>(rb, BS(0), ldb, N, ke, n0, kb, wid, lane);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      glds_tile<ALAY>(ra, AS(cur ^ 1), lda, M, ke, m0, kb + (long)(kt + 1) * BK, wid, lane);
-      glds_tile<BLAY>(rb, BS(cur ^ 1), ldb, N, ke, n0, kb + (long)(kt + 1) * BK, wid, lane);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this tile's 8 DMAs done, next 8 in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // LDS-DMA, NST stages: NST-1 tiles' DMA in flight while one computes; counted vmcnt (8 DMAs per
+  // tile per wave) + raw barriers (a __syncthreads() would drain the in-flight DMA with vmcnt(0), guide §5)
+  constexpr int PF = NST - 1;
+#pragma unroll
+  for (int t = 0; t < PF; ++t)
+    if (t < nk) {
+      glds_tile<ALAY>(ra, AS(t), lda, M, ke, m0, kb + (long)t * BK, wid, lane);
+      glds_tile<BLAY>(rb, BS(t), ldb, N, ke, n0, kb + (long)t * BK, wid, lane);
     }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt % NST;
+    if (kt + PF < nk) {  // refills the buffer computed in iteration kt-1 (behind its closing barrier)
+      const int nb = (kt + PF) % NST;
+      glds_tile<ALAY>(ra, AS(nb), lda, M, ke, m0, kb + (long)(kt + PF) * BK, wid, lane);
+      glds_tile<BLAY>(rb, BS(nb), ldb, N, ke, n0, kb + (long)(kt + PF) * BK, wid, lane);
+    }
+    wait_tiles<NST>(min(nk - 1 - kt, PF));
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
     compute(cur);
     __builtin_amdgcn_s_barrier();  // every wave is done reading buffer cur before it is refilled
@@ -329,14 +349,59 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     }
   }
   __syncthreads();
+  // In-launch split-K combine (tile_cnt != NULL): every slice stores its fp32 partial tile as a
+  // write-through (sc1) slab, drains, and draws a ticket from the tile's counter; the slice that
+  // draws ksplit-1 acquires, sums the slabs in slice order (its own from LDS: the same bits) and
+  // runs the full epilogue, so the result does not depend on arrival order. It also re-zeroes the
+  // counter for the next launch (the caller zero-fills the workspace once).
+  if (tile_cnt) {
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)ws, (short)0, (int)ws_bytes, 0x00020000);
+    const int slab = (split * ntiles + bid) * (BM * BN);
+#pragma unroll 4
+    for (int pass = 0; pass < (BM * BN / 4) / 256; ++pass) {
+      const int id = pass * 256 + tid;
+      const int r = id >> 5, c4 = (id & 31) * 4;
+      const f32x4 v = *(const f32x4*)(cs + r * CST + c4);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rw, (slab + r * BN + c4) * 4, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)(smem + BM * CST * 4);
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(tile_cnt + bid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == ksplit - 1;
+      if (last) {
+        __hip_atomic_store(tile_cnt + bid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+  }
 #pragma unroll 2
   for (int pass = 0; pass < (BM * BN / 8) / 256; ++pass) {
     const int id = pass * 256 + tid;
     const int r = id >> 4, c8 = (id & 15) * 8;
     const long gr = m0 + r, gc = n0 + c8;
     if (gr >= M || gc >= N) continue;
-    const f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
-    if (ksplit > 1) {  // raw fp32 partial slab; gemm_splitk_reduce applies the (plain) epilogue
+    f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
+    if (tile_cnt) {
+      f32x4 sl = {0.f, 0.f, 0.f, 0.f}, sh = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < ksplit; ++k) {
+        if (k == split) {
+          sl += lo;
+          sh += hi;
+        } else {
+          const float* p = ws + (long)(k * ntiles + bid) * (BM * BN) + r * BN + c8;
+          sl += *(const f32x4*)p;
+          sh += *(const f32x4*)(p + 4);
+        }
+      }
+      lo = sl;
+      hi = sh;
+    } else if (ksplit > 1) {  // raw fp32 partial slab; gemm_splitk_reduce applies the (plain) epilogue
       f32x4* o = (f32x4*)(ws + ((long)split * M + gr) * N + gc);
       o[0] = lo;
       o[1] = hi;
@@ -673,7 +738,27 @@ int splitk_plan(long M, long N, long K, long* kchunk) {
   *kchunk = kc;
   return (int)((K + kc - 1) / kc);
 }
-long splitk_ws_bytes(long M, long N, int s) { return s > 1 ? 4L * s * M * N + 4L * s * M : 0; }
+long splitk_ws_bytes(long M, long N, int s) { return s > 1 ? 4096 + 4L * s * M * N + 4L * s * M : 0; }
+
+// split-K with the in-launch combine (any epilogue): grids of <= 128 output tiles -- the d_model =
+// 512 decoder GEMMs (M = B*T rows, N = 512: 128 tiles on 256 CUs) -- cut K so that about one block
+// runs per CU. Per-block latency, not throughput, bounds these.
+int fused_plan(long M, long N, long K, long* kchunk) {
+  const long tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  *kchunk = K;
+  if (tiles > 128 || N % 8) return 1;
+  long s = min(256 / tiles, K / 768);  // the combine costs ~4-5 us: only slices >= 12 K-tiles pay
+  s = min(s, 8L);
+  if (s < 2) return 1;
+  long kc = (K + s - 1) / s;
+  kc = (kc + BK - 1) / BK * BK;
+  *kchunk = kc;
+  return (int)((K + kc - 1) / kc);
+}
+long fused_ws_bytes(long M, long N, int s) {
+  const long tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  return s > 1 ? 4096 + 4L * s * tiles * BM * BN : 0;
+}
 
 // ------------------------------------------------------------------------------------------------
 // fp32 FMA kernel (parity mode): 64x64x16 tile, 256 threads x (4x4) outputs
@@ -743,23 +828,38 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 // ------------------------------------------------------------------------------------------------
 // host side: kernel / epilogue-instance selection
 // ------------------------------------------------------------------------------------------------
+
 template <typename KernelT>
 void set_lds(KernelT k, int bytes) {
   (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
+// split-K decision for a bf16 GEMM on the 128x128 kernel. The workspace's first WS_HDR bytes hold
+// the in-launch combine's per-tile counters; slabs follow.
+constexpr long WS_HDR = 4096;
+struct Split {
+  int ks = 1;
+  long kchunk = 0;
+  bool fused = false;
+};
+
 template <int AL, int BL, int ACT, bool DROP>
-void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, int ksplit, long kchunk,
-                 hipStream_t s) {
+void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, const Split& sp, hipStream_t s) {
+  const int ksplit = sp.ks;
+  const long kchunk = sp.ks > 1 ? sp.kchunk : g->K;
+  float* ws = g->workspace ? (float*)((char*)g->workspace + WS_HDR) : nullptr;
+  int* cnt = sp.fused ? (int*)g->workspace : nullptr;
+  const long wsb = g->workspace ? max(0L, min(g->workspace_bytes - WS_HDR, (long)INT32_MAX)) : 0;
   const long nbm = (g->M + BM - 1) / BM, nbn = (g->N + BN - 1) / BN;
+  const long nblk = nbm * nbn * ksplit;
   static bool attr = false;
   if (!attr) {
-    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP>, SMEM_BYTES);
+    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 2>, smem_bytes(2));
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP>), dim3((unsigned)(nbm * nbn * ksplit)), dim3(256), SMEM_BYTES,
-                     s, (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                     b_bytes, e, ksplit, kchunk, (float*)g->workspace, g->rowsum);
+  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP, 2>), dim3((unsigned)nblk), dim3(256), smem_bytes(2), s,
+                     (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                     b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
 }
 
 template <int AL, int BL, int ACT, bool DROP>
@@ -814,7 +914,7 @@ EpiKind epi_kind(const mit_gemm_args* g) {
 }
 
 template <int AL, int BL>
-void launch_layout(const mit_gemm_args* g, const Epi& e, int ab, int bb, int ks, long kchunk, bool big, hipStream_t s) {
+void launch_layout(const mit_gemm_args* g, const Epi& e, int ab, int bb, const Split& sp, bool big, hipStream_t s) {
   const EpiKind k = epi_kind(g);
   if (big && k != EK_GENERIC) {
     if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
@@ -830,16 +930,16 @@ void launch_layout(const mit_gemm_args* g, const Epi& e, int ab, int bb, int ks,
   }
   if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
     switch (k) {
-      case EK_PLAIN: return launch_bf16<AL, BL, MIT_ACT_NONE, false>(g, e, ab, bb, ks, kchunk, s);
-      case EK_RELU: return launch_bf16<AL, BL, MIT_ACT_RELU, false>(g, e, ab, bb, ks, kchunk, s);
-      case EK_RELU_DROP: return launch_bf16<AL, BL, MIT_ACT_RELU, true>(g, e, ab, bb, ks, kchunk, s);
-      case EK_GELU: return launch_bf16<AL, BL, MIT_ACT_GELU, false>(g, e, ab, bb, ks, kchunk, s);
-      case EK_QGELU: return launch_bf16<AL, BL, MIT_ACT_QUICK_GELU, false>(g, e, ab, bb, ks, kchunk, s);
-      default: return launch_bf16<AL, BL, ACT_RT, true>(g, e, ab, bb, ks, kchunk, s);
+      case EK_PLAIN: return launch_bf16<AL, BL, MIT_ACT_NONE, false>(g, e, ab, bb, sp, s);
+      case EK_RELU: return launch_bf16<AL, BL, MIT_ACT_RELU, false>(g, e, ab, bb, sp, s);
+      case EK_RELU_DROP: return launch_bf16<AL, BL, MIT_ACT_RELU, true>(g, e, ab, bb, sp, s);
+      case EK_GELU: return launch_bf16<AL, BL, MIT_ACT_GELU, false>(g, e, ab, bb, sp, s);
+      case EK_QGELU: return launch_bf16<AL, BL, MIT_ACT_QUICK_GELU, false>(g, e, ab, bb, sp, s);
+      default: return launch_bf16<AL, BL, ACT_RT, true>(g, e, ab, bb, sp, s);
     }
   }
-  if (k == EK_PLAIN) return launch_bf16<AL, BL, MIT_ACT_NONE, false>(g, e, ab, bb, ks, kchunk, s);
-  return launch_bf16<AL, BL, ACT_RT, true>(g, e, ab, bb, ks, kchunk, s);
+  if (k == EK_PLAIN) return launch_bf16<AL, BL, MIT_ACT_NONE, false>(g, e, ab, bb, sp, s);
+  return launch_bf16<AL, BL, ACT_RT, true>(g, e, ab, bb, sp, s);
 }
 
 template <int AL, int BL>
@@ -851,6 +951,38 @@ void launch_f32(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
 
 inline bool al16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 
+int g_fused = -1;  // in-launch split-K combine: -1 = from env on first use
+
+Split plan_split(const mit_gemm_args* g) {
+  Split p;
+  p.kchunk = g->K;
+  if (!g->workspace || !al16(g->workspace)) return p;
+  const bool plain = !g->bias && g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f;
+  long kc;
+  if (plain && g->ldc % 4 == 0 && al16(g->C)) {
+    const int s = splitk_plan(g->M, g->N, g->K, &kc);
+    if (s > 1 && splitk_ws_bytes(g->M, g->N, s) <= g->workspace_bytes) {
+      p.ks = s;
+      p.kchunk = kc;
+      return p;
+    }
+  }
+  // off by default: in the train step the 128-block decoder GEMMs share the chip with the encoder
+  // prefetch and weight-gradient streams, and splitting them measured 0.6 % slower end to end
+  // (9645 vs 9700 pairs/s) though 8-18 % faster alone. MIT_GEMM_FUSED_SPLIT=1 or
+  // mit_gemm_set_fused_split(1) enables it.
+  if (g_fused < 0) g_fused = getenv("MIT_GEMM_FUSED_SPLIT") && atoi(getenv("MIT_GEMM_FUSED_SPLIT")) != 0;
+  if (g_fused && !g->rowsum && !use_256(g->M, g->N, g->K, g->a_layout)) {
+    const int s = fused_plan(g->M, g->N, g->K, &kc);
+    if (s > 1 && fused_ws_bytes(g->M, g->N, s) <= g->workspace_bytes) {
+      p.ks = s;
+      p.kchunk = kc;
+      p.fused = true;
+    }
+  }
+  return p;
+}
+
 }  // namespace
 
 extern "C" int mit_gemm_set_variant(int v) {
@@ -859,26 +991,26 @@ extern "C" int mit_gemm_set_variant(int v) {
   return MIT_OK;
 }
 
+extern "C" int mit_gemm_set_fused_split(int on) {
+  MIT_CHECK_ARG(on == 0 || on == 1, "mit_gemm_set_fused_split: %d not in {0,1}", on);
+  g_fused = on;
+  return MIT_OK;
+}
+
 extern "C" long mit_gemm_workspace_bytes(long M, long N, long K) {
   long kc;
-  return splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc));
+  const long a = splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc));
+  const long b = fused_ws_bytes(M, N, fused_plan(M, N, K, &kc));
+  return a > b ? a : b;
 }
 
 extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
   if (ksplit) *ksplit = 1;
   if (!g || g->M <= 0 || g->N <= 0) return 0;
   if (g->dtype != MIT_BF16) return 64;
-  long kchunk = g->K;
-  int ks = 1;
-  const bool plain = !g->bias && g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f;
-  if (plain && g->workspace) {
-    ks = splitk_plan(g->M, g->N, g->K, &kchunk);
-    if (ks > 1 && (splitk_ws_bytes(g->M, g->N, ks) > g->workspace_bytes || !al16(g->workspace) || g->ldc % 4 != 0 ||
-                   !al16(g->C)))
-      ks = 1;
-  }
-  if (ksplit) *ksplit = ks;
-  const bool big = ks == 1 && use_256(g->M, g->N, g->K, g->a_layout) && epi_kind(g) != EK_GENERIC;
+  const Split sp = plan_split(g);
+  if (ksplit) *ksplit = sp.ks;
+  const bool big = sp.ks == 1 && use_256(g->M, g->N, g->K, g->a_layout) && epi_kind(g) != EK_GENERIC;
   return big ? 256 : 128;
 }
 
@@ -932,29 +1064,20 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (g->dtype == MIT_BF16) {
     const int ab = (int)a_bytes, bb = (int)b_bytes;
-    long kchunk = g->K;
-    int ks = 1;
-    const bool plain = !g->bias && g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f;
-    if (plain && g->workspace) {
-      ks = splitk_plan(g->M, g->N, g->K, &kchunk);
-      if (ks > 1 && (splitk_ws_bytes(g->M, g->N, ks) > g->workspace_bytes || !al16(g->workspace) ||
-                     g->ldc % 4 != 0 || !al16(g->C))) {
-        ks = 1;
-        kchunk = g->K;
-      }
-    }
-    const bool big = ks == 1 && use_256(g->M, g->N, g->K, g->a_layout);
-    if (g->a_layout == 0 && g->b_layout == 0) launch_layout<0, 0>(g, e, ab, bb, ks, kchunk, big, s);
-    else if (g->a_layout == 0 && g->b_layout == 1) launch_layout<0, 1>(g, e, ab, bb, ks, kchunk, big, s);
-    else if (g->a_layout == 1 && g->b_layout == 0) launch_layout<1, 0>(g, e, ab, bb, ks, kchunk, big, s);
-    else launch_layout<1, 1>(g, e, ab, bb, ks, kchunk, big, s);
-    if (ks > 1) {
+    const Split sp = plan_split(g);
+    const bool big = sp.ks == 1 && use_256(g->M, g->N, g->K, g->a_layout);
+    if (g->a_layout == 0 && g->b_layout == 0) launch_layout<0, 0>(g, e, ab, bb, sp, big, s);
+    else if (g->a_layout == 0 && g->b_layout == 1) launch_layout<0, 1>(g, e, ab, bb, sp, big, s);
+    else if (g->a_layout == 1 && g->b_layout == 0) launch_layout<1, 0>(g, e, ab, bb, sp, big, s);
+    else launch_layout<1, 1>(g, e, ab, bb, sp, big, s);
+    if (sp.ks > 1 && !sp.fused) {
       MIT_LAUNCH_CHECK("mit_gemm");
       const long total = g->M * (g->N / 4);
       long blocks = (total + 255) / 256;
       if (blocks > 4096) blocks = 4096;
-      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, g->M, g->N, ks,
-                         (const float*)g->workspace, g->C, g->ldc, g->alpha, g->out_f32, g->accumulate, g->rowsum);
+      hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, g->M, g->N, sp.ks,
+                         (const float*)((char*)g->workspace + WS_HDR), g->C, g->ldc, g->alpha, g->out_f32,
+                         g->accumulate, g->rowsum);
     }
   } else {
     if (g->a_layout == 0 && g->b_layout == 0) launch_f32<0, 0>(g, e, s);

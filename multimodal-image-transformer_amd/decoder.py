@@ -152,6 +152,16 @@ class _Acts:
         self.count = f(1)
         self.loss_sum = f(1)
         self.loss = f(1)
+        # split-K scratch of the main stream: the d_model GEMMs (R x d outputs, 128 tiles at B = 64)
+        # combine their K slices in-launch; weight-gradient / long-K GEMMs reduce in a second launch.
+        # Zero-filled once: its first 4 KiB are tile counters the kernels leave at zero.
+        E = proj_in or d
+        shapes = [(R, d, d), (R, d, F), (R, d, 3 * d), (R, d, V)]
+        if train:
+            shapes += [(V, d, R), (d, F, R), (F, d, R), (d, d, R), (3 * d, d, R), (L * 2 * d, d, B * S), (d, E, B * S),
+                       (B * S, d, L * 2 * d)]
+        need = max(native.gemm_workspace_bytes(m, n, k) for m, n, k in shapes)
+        self.gemm_ws = torch.zeros(max(need, 4096) // 4 + 4, dtype=torch.float32, device=dev)
         if train:
             self.dx = e(R, d)
             self.dy = e(R, d)
@@ -163,14 +173,8 @@ class _Acts:
             self.dmem = e(B * S, d)
             self.delta = f(B * H * T)
             self.ln_ws = f(native.layernorm_bwd_ws_floats(R, d))
-            # split-K scratch for the weight-gradient GEMMs (and the long-K dX GEMMs)
-            E = proj_in or d
-            shapes = [(V, d, R), (d, F, R), (F, d, R), (d, d, R), (3 * d, d, R), (L * 2 * d, d, B * S), (d, E, B * S),
-                      (R, d, V), (B * S, d, L * 2 * d)]
-            need = max(native.gemm_workspace_bytes(m, n, k) for m, n, k in shapes)
-            self.gemm_ws = torch.empty(max(need, 16) // 4 + 4, dtype=torch.float32, device=dev)
             # the weight-gradient GEMMs run on a side stream (_SideStream) with their own scratch
-            self.gemm_ws_side = torch.empty(max(need, 16) // 4 + 4, dtype=torch.float32, device=dev)
+            self.gemm_ws_side = torch.zeros(max(need, 4096) // 4 + 4, dtype=torch.float32, device=dev)
 
 
 class _SideStream:
@@ -350,6 +354,7 @@ class TransformerDecoder:
         p = drop_p if drop_p is not None else (self._p() if train else 0.0)
         w = st.w
         R = B * T
+        ws = A.gemm_ws
         # fused cross-attention K/V projection of every layer (decoder-layer independent)
         native.gemm(mem, w("cross_kv.weight"), A.kv, B * S, L * 2 * d, d, lda=mem_ld, bias=st.p("cross_kv.bias"))
         native.embed_fwd(tokens, w("token_embedding.weight"), math.sqrt(d), self.pe, A.x0, drop_p=p, seed=seed,
@@ -368,21 +373,21 @@ class TransformerDecoder:
                                   pad_idx=self.pad_idx, causal=True, scale=1.0 / math.sqrt(64), drop_p=p, seed=seed,
                                   site=base + 0)
             native.attention_fwd(native.dtype_code(qkv), B, H, T, T, sa)
-            native.linear(A.os[j], w(pre + "self_out.weight"), A.y, bias=st.p(pre + "self_out.bias"))
+            native.linear(A.os[j], w(pre + "self_out.weight"), A.y, bias=st.p(pre + "self_out.bias"), workspace=ws)
             native.layernorm_fwd(xin, st.p(pre + "norm1.weight"), st.p(pre + "norm1.bias"), 1e-5, xs[0], r=A.y,
                                  drop_p=p, seed=seed, site=base + 1, z=z[0], mean=stt[0][0], rstd=stt[0][1])
-            native.linear(xs[0], w(pre + "cross_q.weight"), A.qc[j], bias=st.p(pre + "cross_q.bias"))
+            native.linear(xs[0], w(pre + "cross_q.weight"), A.qc[j], bias=st.p(pre + "cross_q.bias"), workspace=ws)
             kvl = A.kv[:, l * 2 * d:]
             ca = native.attn_args(A.qc[j], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
                                   S * L * 2 * d, A.oc[j], d, T * d, lse=A.lse_c[j], scale=1.0 / math.sqrt(64), drop_p=p,
                                   seed=seed, site=base + 2)
             native.attention_fwd(native.dtype_code(qkv), B, H, T, S, ca)
-            native.linear(A.oc[j], w(pre + "cross_out.weight"), A.y, bias=st.p(pre + "cross_out.bias"))
+            native.linear(A.oc[j], w(pre + "cross_out.weight"), A.y, bias=st.p(pre + "cross_out.bias"), workspace=ws)
             native.layernorm_fwd(xs[0], st.p(pre + "norm2.weight"), st.p(pre + "norm2.bias"), 1e-5, xs[1], r=A.y,
                                  drop_p=p, seed=seed, site=base + 3, z=z[1], mean=stt[1][0], rstd=stt[1][1])
             native.linear(xs[1], w(pre + "linear1.weight"), A.h[j], bias=st.p(pre + "linear1.bias"),
                           act=native.ACT_RELU, drop_p=p, seed=seed, site=base + 4)
-            native.linear(A.h[j], w(pre + "linear2.weight"), A.y, bias=st.p(pre + "linear2.bias"))
+            native.linear(A.h[j], w(pre + "linear2.weight"), A.y, bias=st.p(pre + "linear2.bias"), workspace=ws)
             native.layernorm_fwd(xs[1], st.p(pre + "norm3.weight"), st.p(pre + "norm3.bias"), 1e-5, xs[2], r=A.y,
                                  drop_p=p, seed=seed, site=base + 5, z=z[2], mean=stt[2][0], rstd=stt[2][1])
             xin = xs[2]
@@ -450,7 +455,8 @@ class TransformerDecoder:
             native.gemm(A.dy, w(pre + "linear2.weight"), A.dh, R, F, d, b_layout=MN, ldb=F, aux=A.h[l], ld_aux=F,
                         aux_scale=ascale)
             dW(A.dh, xs[1], pre + "linear1.weight", pre + "linear1.bias", F, d, R, F, d)
-            native.gemm(A.dh, w(pre + "linear1.weight"), A.dx, R, d, F, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
+            native.gemm(A.dh, w(pre + "linear1.weight"), A.dx, R, d, F, b_layout=MN, ldb=d, residual=A.dx, ldr=d,
+                        workspace=ws)
             # LN2
             guard(A.dy)
             native.layernorm_bwd(A.dx, z[1], stt[1][0], stt[1][1], st.p(pre + "norm2.weight"), A.dx,
@@ -458,7 +464,7 @@ class TransformerDecoder:
                                  site=base + 3)
             # cross-attention block
             dW(A.dy, A.oc[l], pre + "cross_out.weight", pre + "cross_out.bias", d, d, R, d, d)
-            native.gemm(A.dy, w(pre + "cross_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d)
+            native.gemm(A.dy, w(pre + "cross_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)
             kvl, dkvl = A.kv[:, l * 2 * d:], A.dkv[:, l * 2 * d:]
             ca = native.attn_args(A.qc[l], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
                                   S * L * 2 * d, A.oc[l], d, T * d, lse=A.lse_c[l], scale=1.0 / math.sqrt(64), drop_p=p,
@@ -468,7 +474,8 @@ class TransformerDecoder:
             guard(A.dq)
             native.attention_bwd(native.dtype_code(A.dq), B, H, T, S, ca, cg)
             dW(A.dq, xs[0], pre + "cross_q.weight", pre + "cross_q.bias", d, d, R, d, d)
-            native.gemm(A.dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
+            native.gemm(A.dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d,
+                        workspace=ws)
             # LN1
             guard(A.dy)
             native.layernorm_bwd(A.dx, z[0], stt[0][0], stt[0][1], st.p(pre + "norm1.weight"), A.dx,
@@ -476,7 +483,7 @@ class TransformerDecoder:
                                  site=base + 1)
             # self-attention block
             dW(A.dy, A.os[l], pre + "self_out.weight", pre + "self_out.bias", d, d, R, d, d)
-            native.gemm(A.dy, w(pre + "self_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d)
+            native.gemm(A.dy, w(pre + "self_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)
             qkv = A.qkv[l]
             sa = native.attn_args(qkv, 3 * d, T * 3 * d, qkv[:, d:], 3 * d, T * 3 * d, qkv[:, 2 * d:], 3 * d, T * 3 * d,
                                   A.os[l], d, T * d, lse=A.lse_s[l], key_tokens=tokens, tok_batch=T,
@@ -487,7 +494,8 @@ class TransformerDecoder:
             guard(A.dqkv)
             native.attention_bwd(native.dtype_code(A.dq), B, H, T, T, sa, sg)
             dW(A.dqkv, xin, pre + "self_in.weight", pre + "self_in.bias", 3 * d, d, R, 3 * d, d)
-            native.gemm(A.dqkv, w(pre + "self_in.weight"), A.dx, R, d, 3 * d, b_layout=MN, ldb=d, residual=A.dx, ldr=d)
+            native.gemm(A.dqkv, w(pre + "self_in.weight"), A.dx, R, d, 3 * d, b_layout=MN, ldb=d, residual=A.dx,
+                        ldr=d, workspace=ws)
             ready(pre + "linear2.weight", pre + "norm1.bias")
         # cross K/V of all layers
         BS = B * S

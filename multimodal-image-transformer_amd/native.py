@@ -65,6 +65,7 @@ SIGNATURES = {
     "mit_gemm_workspace_bytes": (L, [L, L, L]),
     "mit_gemm_set_variant": (I, [I]),
     "mit_gemm_plan": (I, [ctypes.POINTER(GemmArgs), ctypes.POINTER(I)]),
+    "mit_gemm_set_fused_split": (I, [I]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
@@ -151,7 +152,8 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
          act=ACT_NONE, residual=None, ldr=None, aux=None, ld_aux=None, aux_scale=1.0, alpha=1.0, drop_p=0.0,
          seed=None, site=0, accumulate=False, rowsum=None, workspace=None):
     """C = epi(alpha * A(m,k) B(k,n)); see include/mit_hip.h. Output dtype = C.dtype (f32 or operand dtype).
-    rowsum: optional f32 [M] <- sum_k A(m,k) (fused bias gradient); workspace: split-K scratch."""
+    rowsum: optional f32 [M] <- sum_k A(m,k) (fused bias gradient); workspace: split-K scratch, zero-filled
+    once before first use (gemm_workspace(M, N, K)), one per stream."""
     dt = dtype_code(A)
     if B.dtype != A.dtype:
         raise NativeError("gemm: A and B dtypes differ")
@@ -200,6 +202,11 @@ def gemm_set_variant(v):
     _check(lib().mit_gemm_set_variant(int(v)), "mit_gemm_set_variant")
 
 
+def gemm_set_fused_split(on):
+    """In-launch split-K combine for the <= 128-tile GEMMs (off by default)."""
+    _check(lib().mit_gemm_set_fused_split(1 if on else 0), "mit_gemm_set_fused_split")
+
+
 def gemm_plan(g):
     """(tile edge, split-K factor) of the launch mit_gemm would make for recorded args g."""
     ks = ctypes.c_int(1)
@@ -211,12 +218,17 @@ def gemm_workspace_bytes(M, N, K):
     return lib().mit_gemm_workspace_bytes(M, N, K)
 
 
-def linear(x, w, out, *, bias=None, act=ACT_NONE, residual=None, drop_p=0.0, seed=None, site=0):
+def gemm_workspace(M, N, K, device=None):
+    """A zero-filled split-K workspace big enough for an (M, N, K) GEMM."""
+    return torch.zeros(max(gemm_workspace_bytes(M, N, K), 4096) // 4 + 4, dtype=torch.float32, device=device)
+
+
+def linear(x, w, out, *, bias=None, act=ACT_NONE, residual=None, drop_p=0.0, seed=None, site=0, workspace=None):
     """out[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual) — nn.Linear forward."""
     M, K = x.shape[0], x.shape[-1]
     N = w.shape[0]
     gemm(x, w, out, M, N, K, lda=x.stride(0), bias=bias, act=act, residual=residual, drop_p=drop_p, seed=seed,
-         site=site)
+         site=site, workspace=workspace)
 
 
 def layernorm_fwd(x, gamma, beta, eps, y, *, r=None, drop_p=0.0, seed=None, site=0, z=None, mean=None, rstd=None,

@@ -21,6 +21,7 @@ def _lib():
     N.load_library()
     yield
     N.gemm_set_variant(0)
+    N.gemm_set_fused_split(0)
 
 
 def _ops(M, Nn, K, al, bl, seed=0):
@@ -124,3 +125,43 @@ def test_gemm_gelu_epilogue_accuracy():
         N.gemm(x, w, out, M, Nn, K, bias=bias, act=N.ACT_GELU)
         err = (out.double() - ref).abs().max().item()
         assert err < 2e-5 * ref.abs().max().item(), (v, err)
+
+
+@pytest.mark.parametrize("al,bl", [(0, 0), (0, 1)])
+@pytest.mark.parametrize("M,Nn,K", [(4032, 512, 1536), (4032, 512, 2048), (1000, 520, 3072), (200, 136, 4096)])
+@pytest.mark.parametrize("epi", ["plain", "bias_res", "relu_drop", "aux_f32acc", "gelu"])
+def test_gemm_split_k_in_launch_combine(al, bl, M, Nn, K, epi):
+    """Split-K with the in-launch combine (<= 128 output tiles, any epilogue): equal to the same
+    GEMM without a workspace (no split) up to fp32 summation order, bit-identical over repeats
+    (the combine sums slabs in slice order whatever the arrival order), counters left at zero."""
+    N.gemm_set_fused_split(1)
+    A, B, ref = _ops(M, Nn, K, al, bl, seed=M + K)
+    g = torch.Generator().manual_seed(3)
+    kw = {}
+    out_dt = torch.bfloat16
+    if epi == "bias_res":
+        kw = dict(bias=torch.randn(Nn, generator=g).to(dev()), residual=torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16))
+    elif epi == "relu_drop":
+        kw = dict(act=N.ACT_RELU, drop_p=0.25, seed=torch.tensor([11], device=dev()), site=3)
+    elif epi == "aux_f32acc":
+        kw = dict(aux=torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16), aux_scale=1.5, accumulate=True)
+        out_dt = torch.float32
+    elif epi == "gelu":
+        kw = dict(act=N.ACT_GELU, bias=torch.randn(Nn, generator=g).to(dev()))
+    ws = N.gemm_workspace(M, Nn, K, dev())
+    args = N.GemmArgs(N.BF16, al, bl, M, Nn, K, A.data_ptr(), K if al == 0 else M, B.data_ptr(),
+                      K if bl == 0 else Nn, 0, Nn, 1.0, None, 0, None, Nn, None, Nn, 1.0, 0.0, None, 0, 0, 0, None,
+                      ws.data_ptr(), ws.numel() * 4)
+    tile, ks = N.gemm_plan(args)
+    assert tile == 128 and ks >= 2, (tile, ks)
+    base = torch.randn(M, Nn, generator=g).to(dev(), out_dt)
+    outs = []
+    for w in (None, ws, ws, ws):
+        C = base.clone()
+        N.gemm(A, B, C, M, Nn, K, a_layout=al, b_layout=bl, workspace=w, **kw)
+        outs.append(C)
+    assert torch.equal(outs[1], outs[2]) and torch.equal(outs[1], outs[3])
+    assert torch.count_nonzero(ws[:1024]).item() == 0
+    d = (outs[1].float() - outs[0].float()).abs().max().item()
+    scale = max(outs[0].float().abs().max().item(), 1.0)
+    assert d <= (2e-2 if out_dt == torch.bfloat16 else 1e-4) * scale, d

@@ -269,7 +269,7 @@ def test_encoder_prefetch_matches_inline():
 
 def test_checkpoint_save_resume_roundtrip(tmp_path):
     """train.save_checkpoint -> train.load_checkpoint (train.py:343-375, 412-442): a resumed model
-    continues EXACTLY where the original left off (weights, AdamW moments, step count, scheduler);
+    continues where the original left off (weights, AdamW moments, step count, scheduler);
     the .safetensors restores weights only (inference.py:66-67)."""
     import optim
     import train as TR
@@ -299,8 +299,9 @@ def test_checkpoint_save_resume_roundtrip(tmp_path):
     m2, opt2, sch2 = fresh()
     start, best = TR.load_checkpoint(m2, opt2, sch2, name + ".pt")
     assert start == 1 and abs(best - 1.2345) < 1e-9
-    assert step(m2, opt2, sch2, batches[2]) == ref_next
-    torch.testing.assert_close(m2.store.master, ref_params, rtol=0, atol=0)
+    # up to float-atomic summation order (the embedding-gradient scatter-add)
+    assert abs(step(m2, opt2, sch2, batches[2]) - ref_next) <= 1e-5 * abs(ref_next)
+    torch.testing.assert_close(m2.store.master, ref_params, rtol=1e-5, atol=1e-6)
 
     m3, opt3, sch3 = fresh()
     assert TR.load_checkpoint(m3, opt3, sch3, name + ".safetensors") == (0, float("inf"))

@@ -16,6 +16,12 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("4096^3", 4096, 4096, 4096, 0, 0),
     ("enc fc1+gelu", 12608, 3072, 768, 0, 0, "gelu"), ("enc fc2+res", 12608, 768, 3072, 0, 0, "res"),
     ("enc qkv+bias", 12608, 2304, 768, 0, 0, "bias"), ("dec ffn1+relu+drop", 4032, 2048, 512, 0, 0, "reludrop"),
+    # the d_model = 512 decoder GEMMs (128 output tiles)
+    ("fwd out+bias", 4032, 512, 512, 0, 0, "bias"), ("fwd lin2+res", 4032, 512, 2048, 0, 0, "res"),
+    ("dX out", 4032, 512, 512, 0, 1), ("dX q+res", 4032, 512, 512, 0, 1, "res0"),
+    ("dX lin1+res", 4032, 512, 2048, 0, 1, "res0"), ("dX self_in+res", 4032, 512, 1536, 0, 1, "res0"),
+    ("dX fc_out ws", 4032, 512, 10000, 0, 1, "ws"), ("dW dd ws", 512, 512, 4032, 1, 1, "ws"),
+    ("dW ffn ws", 2048, 512, 4032, 1, 1, "ws"),
 ]
 
 
@@ -33,7 +39,12 @@ def run(iters=20, variants=(1, 2)):
         out_f32 = al == 1
         C = torch.empty(M, N, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
         kw = {}
-        if epi:
+        ws = native.gemm_workspace(M, N, K, dev)  # as the train step passes it (split-K when planned)
+        if epi == "ws":
+            pass
+        elif epi == "res0":
+            kw["residual"] = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        elif epi:
             kw["bias"] = torch.randn(N, device=dev)
         if epi == "gelu":
             kw["act"] = native.ACT_GELU
@@ -43,15 +54,16 @@ def run(iters=20, variants=(1, 2)):
             kw.update(act=native.ACT_RELU, drop_p=0.1, seed=torch.tensor([7], device=dev), site=1)
         best = {}
         for rnd in range(3):  # interleaved rounds, one process (guide §5.4 rule 24)
-            for v in variants:
-                native.gemm_set_variant(v)
+            for v in variants:  # "<variant>" with the workspace, "<variant>n" without (no split-K)
+                native.gemm_set_variant(int(v.rstrip("n")))
+                kv = dict(kw, workspace=None if v.endswith("n") else ws)
                 for _ in range(3):
-                    native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, **kw)
+                    native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, **kv)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(iters):
-                    native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, **kw)
+                    native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, **kv)
                 e1.record()
                 torch.cuda.synchronize()
                 t = e0.elapsed_time(e1) / iters * 1e-3
@@ -61,7 +73,7 @@ def run(iters=20, variants=(1, 2)):
             t = best[v]
             tf = 2 * M * N * K / t / 1e12
             res.append((name, v, M, N, K, t * 1e6, tf))
-            line += f"  v{v} {t*1e6:8.1f} us {tf:7.1f} TF"
+            line += f"  v{v:3s} {t*1e6:8.1f} us {tf:7.1f} TF"
         print(line, flush=True)
     native.gemm_set_variant(0)
     return res
@@ -69,5 +81,5 @@ def run(iters=20, variants=(1, 2)):
 
 if __name__ == "__main__":
     native.load_library()
-    vs = tuple(int(v) for v in sys.argv[1].split(",")) if len(sys.argv) > 1 else (1, 2)
+    vs = tuple(sys.argv[1].split(",")) if len(sys.argv) > 1 else ("1", "2")
     run(variants=vs)
