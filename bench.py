@@ -152,7 +152,8 @@ class GemmProbe:
 
 
 def pmc_traffic(kernel_prefix):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC summary (FETCH_SIZE and
+    """HBM bytes per launch of a kernel (averaged over the launches of all its template instances)
+    from the committed rocprofv3 PMC summary (FETCH_SIZE and
     WRITE_SIZE passes of tools/profile_r01.sh over this same command, condensed by
     tools/rocpd_summary.py); None when no summary is present."""
     path = os.path.join(ROOT, "profiles", PMC_SUMMARY)
@@ -161,10 +162,13 @@ def pmc_traffic(kernel_prefix):
             ks = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None, None
+    # every template instance of the kernel (activation / dropout variants), launch-weighted
+    tot, n = 0.0, 0
     for name, e in ks.items():
         if name.startswith(kernel_prefix) and "hbm_bytes_per_launch" in e:
-            return e["hbm_bytes_per_launch"], f"profiles/{PMC_SUMMARY}"
-    return None, None
+            tot += e["hbm_bytes_per_launch"] * e["launches"]
+            n += e["launches"]
+    return (round(tot / n), f"profiles/{PMC_SUMMARY}") if n else (None, None)
 
 
 def build(args, rank):
@@ -325,6 +329,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (launches are asynchronous)
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -346,6 +351,8 @@ def main():
                    "memory_mode": args.memory_mode, "parallelism": f"dp{world}",
                    "gflop_per_pair": round(flops_pair / 1e9, 3)},
         "step_mfma_frac": round(value / world * flops_pair / (MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+        # ~ms_per_step when the host's launch path, not the GPU, paces the step
+        "host_enqueue_ms_per_step": round(1e3 * t_enq / args.steps, 3),
         "final_loss": round(loss, 4),
     }
     if not args.no_roofline:

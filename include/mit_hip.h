@@ -114,12 +114,14 @@ int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x, long ldx, 
 
 /* Backward of y = LN(z), z = x + dropout(r):
  *   dx = dz = dLN(dy) (dx may alias dy), dr = dz * dropout_mask (may be NULL)
- *   dgamma/dbeta: f32 [cols], overwritten.
+ *   dgamma/dbeta: f32 [cols], overwritten. Both NULL: the per-block column partials are left in
+ *     ws and mit_layernorm_param_grads reduces them later (e.g. on another stream, off the dX chain).
  *   ws: f32 workspace of >= mit_layernorm_bwd_ws_floats(rows, cols) floats. */
 long mit_layernorm_bwd_ws_floats(long rows, long cols);
 int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy, const void* z, const float* mean,
                       const float* rstd, const float* gamma, void* dx, void* dr, float r_drop_p, const uint64_t* seed,
                       uint32_t site, float* dgamma, float* dbeta, float* ws, void* stream);
+int mit_layernorm_param_grads(long rows, long cols, const float* ws, float* dgamma, float* dbeta, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Scaled-dot-product attention, head_dim 64, heads interleaved inside a token row (column h*64).
@@ -195,10 +197,13 @@ int mit_embed_bwd(int dtype, long B, long T, long d, const int64_t* tokens, cons
  *     if want_grad, logits are overwritten IN PLACE by d(loss)/d(logits) =
  *     (softmax - onehot) / count[0], and by 0 for ignored rows. count is a device scalar (the
  *     GLOBAL non-PAD count: the reference's mean reduction, exact under data parallelism).
+ *     row_loss (f32 [rows], may be NULL): scratch for a deterministic loss sum (per-row losses added
+ *     in row order; bf16 rows with V <= 10240 also take the register-resident one-wave-per-row
+ *     kernel). NULL: per-row float atomics into loss_sum (order-dependent rounding).
  * scalar_div: out[0] = a[0] / b[0] (mean loss = loss_sum / count, on device, no host sync). */
 int mit_count_targets(const int64_t* targets, long n, int ignore_index, float* count, void* stream);
 int mit_cross_entropy(int dtype, long rows, long V, void* logits, long ld, const int64_t* targets, int ignore_index,
-                      const float* count, float* loss_sum, int want_grad, void* stream);
+                      const float* count, float* loss_sum, int want_grad, float* row_loss, void* stream);
 int mit_scalar_div(const float* a, const float* b, float* out, void* stream);
 
 /* bias gradient: out[n] (+)= sum_m dy[m*ld + n]  (f32 out; accumulate flag) */

@@ -85,7 +85,7 @@ __global__ void count_kernel(const int64_t* __restrict__ t, long n, int ignore, 
 template <typename T>
 __global__ __launch_bounds__(256) void ce_kernel(long V, T* logits, long ld, const int64_t* __restrict__ targets,
                                                  int ignore, const float* __restrict__ count, float* loss_sum,
-                                                 int want_grad) {
+                                                 int want_grad, float* row_loss) {
   __shared__ float scratch[16];
   const long row = blockIdx.x;
   T* x = logits + row * ld;
@@ -98,7 +98,10 @@ __global__ __launch_bounds__(256) void ce_kernel(long V, T* logits, long ld, con
   for (long j = threadIdx.x; j < V; j += blockDim.x) se += __expf(to_f(x[j]) - mx);
   se = block_sum(se, scratch);
   const float lse = mx + __logf(se);
-  if (threadIdx.x == 0 && !ign) atomicAdd(loss_sum, lse - to_f(x[tg]));
+  if (threadIdx.x == 0) {
+    if (row_loss) row_loss[row] = ign ? 0.f : lse - to_f(x[tg]);
+    else if (!ign) atomicAdd(loss_sum, lse - to_f(x[tg]));
+  }
   if (want_grad) {
     __syncthreads();  // every thread has read x[tg] above before anyone overwrites it
     const float gs = ign ? 0.f : 1.0f / *count;
@@ -109,6 +112,74 @@ __global__ __launch_bounds__(256) void ce_kernel(long V, T* logits, long ld, con
       x[j] = from_f<T>(p * gs);
     }
   }
+}
+
+// bf16 rows with V <= CE_NCH * 512 (the decoder head, V = 10000): one wave per row, the row held in
+// registers (CE_NCH x 16-B loads per lane), so HBM sees one read and one write of the logits; each
+// row's loss goes to row_loss[row] and ce_sum adds them up in row order (deterministic, no
+// single-address float atomics: 4032 of those serialised cost ~100 us).
+constexpr int CE_NCH = 20;
+__global__ __launch_bounds__(256) void ce_rows_bf16(long rows, long V, bf16* logits, long ld,
+                                                     const int64_t* __restrict__ targets, int ignore,
+                                                     const float* __restrict__ count, float* __restrict__ row_loss,
+                                                     int want_grad) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  bf16* x = logits + row * ld;
+  const int64_t tg = targets[row];
+  const bool ign = tg == ignore;
+  bf16x8 v[CE_NCH];
+#pragma unroll
+  for (int c = 0; c < CE_NCH; ++c) {
+    const long j = (long)c * 512 + lane * 8;
+    if (j < V) v[c] = *(const bf16x8*)(x + j);
+  }
+  const float xt = (!ign && tg >= 0 && tg < V) ? (float)x[tg] : 0.f;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < CE_NCH; ++c)
+    if ((long)c * 512 + lane * 8 < V) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mx = fmaxf(mx, (float)v[c][k]);
+    }
+  mx = wave_max(mx);
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < CE_NCH; ++c)
+    if ((long)c * 512 + lane * 8 < V) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) se += __expf((float)v[c][k] - mx);
+    }
+  se = wave_sum(se);
+  const float lse = mx + __logf(se);
+  if (lane == 0) row_loss[row] = ign ? 0.f : lse - xt;
+  if (!want_grad) return;
+  const float gs = ign ? 0.f : 1.0f / *count;
+  const float inv = 1.0f / se;
+#pragma unroll
+  for (int c = 0; c < CE_NCH; ++c) {
+    const long j = (long)c * 512 + lane * 8;
+    if (j < V) {
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float p = __expf((float)v[c][k] - mx) * inv;
+        if (j + k == tg) p -= 1.0f;
+        o[k] = (bf16)(p * gs);
+      }
+      *(bf16x8*)(x + j) = o;
+    }
+  }
+}
+
+// loss_sum += sum(row_loss[0..rows)) in a fixed order (one block)
+__global__ __launch_bounds__(1024) void ce_sum(long rows, const float* __restrict__ row_loss, float* loss_sum) {
+  __shared__ float scratch[16];
+  float s = 0.f;
+  for (long r = threadIdx.x; r < rows; r += blockDim.x) s += row_loss[r];
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) *loss_sum += s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -310,13 +381,27 @@ extern "C" int mit_count_targets(const int64_t* targets, long n, int ignore_inde
 
 extern "C" int mit_cross_entropy(int dtype, long rows, long V, void* logits, long ld, const int64_t* targets,
                                  int ignore_index, const float* count, float* loss_sum, int want_grad,
-                                 void* stream) {
+                                 float* row_loss, void* stream) {
   MIT_CHECK_ARG(logits && targets && loss_sum && (!want_grad || count), "mit_cross_entropy: null pointer");
   MIT_CHECK_ARG(ld >= V, "mit_cross_entropy: ld < V");
   if (rows <= 0) return MIT_OK;
+  if (row_loss && dtype == MIT_BF16 && V <= CE_NCH * 512 && V % 8 == 0 && ld % 8 == 0 &&
+      ((uintptr_t)logits % 16) == 0) {
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(ce_rows_bf16, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, rows, V, (bf16*)logits, ld,
+                       targets, ignore_index, count, row_loss, want_grad);
+    MIT_LAUNCH_CHECK("mit_cross_entropy");
+    hipLaunchKernelGGL(ce_sum, dim3(1), dim3(1024), 0, s, rows, (const float*)row_loss, loss_sum);
+    MIT_LAUNCH_CHECK("mit_cross_entropy(sum)");
+    return MIT_OK;
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(ce_kernel<T>, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, V,
-                                       (T*)logits, ld, targets, ignore_index, count, loss_sum, want_grad));
+                                       (T*)logits, ld, targets, ignore_index, count, loss_sum, want_grad, row_loss));
   MIT_LAUNCH_CHECK("mit_cross_entropy");
+  if (row_loss) {
+    hipLaunchKernelGGL(ce_sum, dim3(1), dim3(1024), 0, (hipStream_t)stream, rows, (const float*)row_loss, loss_sum);
+    MIT_LAUNCH_CHECK("mit_cross_entropy(sum)");
+  }
   return MIT_OK;
 }
 

@@ -224,25 +224,28 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long rows, long cols, const
   }
 }
 
-// column-parallel sum of the block partials: 64 columns x 4 strided partial-row groups per block
+// column-parallel sum of the block partials: 16 columns x 16 strided partial-row groups per block
+// (at 4032 rows x 512 columns: 252 partial rows, 64 blocks, 16 loads in flight per thread), then a
+// fixed-order LDS reduction over the groups (deterministic)
 __global__ __launch_bounds__(256) void ln_param_reduce(long nblk, long cols, const float* __restrict__ ws,
                                                        float* dgamma, float* dbeta) {
-  __shared__ float part[4][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const long c = (long)blockIdx.x * 64 + cl;
+  __shared__ float part[16][17];
+  const int cl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const long c = (long)blockIdx.x * 16 + cl;
   float s = 0.f;
   if (c < 2 * cols) {
     long b = grp;
-    for (; b + 12 < nblk; b += 16) {
-      s += ws[b * 2 * cols + c] + ws[(b + 4) * 2 * cols + c] + ws[(b + 8) * 2 * cols + c] +
-           ws[(b + 12) * 2 * cols + c];
-    }
-    for (; b < nblk; b += 4) s += ws[b * 2 * cols + c];
+    for (; b + 48 < nblk; b += 64)
+      s += (ws[b * 2 * cols + c] + ws[(b + 16) * 2 * cols + c]) +
+           (ws[(b + 32) * 2 * cols + c] + ws[(b + 48) * 2 * cols + c]);
+    for (; b < nblk; b += 16) s += ws[b * 2 * cols + c];
   }
   part[grp][cl] = s;
   __syncthreads();
   if (grp == 0 && c < 2 * cols) {
-    const float t = part[0][cl] + part[1][cl] + part[2][cl] + part[3][cl];
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += part[g][cl];
     if (c < cols) dgamma[c] = t;
     else dbeta[c - cols] = t;
   }
@@ -309,7 +312,8 @@ extern "C" int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy
                                  const uint64_t* seed, uint32_t site, float* dgamma, float* dbeta, float* ws,
                                  void* stream) {
   MIT_CHECK_ARG(cols > 0 && cols <= 64 * MAXV_ALL, "mit_layernorm_bwd: cols %ld out of range", cols);
-  MIT_CHECK_ARG(dy && z && mean && rstd && gamma && dx && dgamma && dbeta && ws, "mit_layernorm_bwd: null pointer");
+  MIT_CHECK_ARG(dy && z && mean && rstd && gamma && dx && ws, "mit_layernorm_bwd: null pointer");
+  MIT_CHECK_ARG(!dgamma == !dbeta, "mit_layernorm_bwd: dgamma and dbeta must both be set or both be NULL");
   if (rows <= 0) return MIT_OK;
   const int dropout = r_drop_p > 0.f;
   const uint32_t th = drop_threshold(r_drop_p);
@@ -337,8 +341,21 @@ extern "C" int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy
     else go(float(), std::false_type());
   }
   MIT_LAUNCH_CHECK("mit_layernorm_bwd");
-  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((2 * cols + 63) / 64)), dim3(256), 0, s, nblk, cols, ws, dgamma,
+  if (!dgamma) return MIT_OK;  // partials stay in ws for mit_layernorm_param_grads
+  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((2 * cols + 15) / 16)), dim3(256), 0, s, nblk, cols, ws, dgamma,
                      dbeta);
   MIT_LAUNCH_CHECK("mit_layernorm_bwd(reduce)");
+  return MIT_OK;
+}
+
+extern "C" int mit_layernorm_param_grads(long rows, long cols, const float* ws, float* dgamma, float* dbeta,
+                                         void* stream) {
+  MIT_CHECK_ARG(ws && dgamma && dbeta, "mit_layernorm_param_grads: null pointer");
+  MIT_CHECK_ARG(cols > 0, "mit_layernorm_param_grads: cols %ld", cols);
+  if (rows <= 0) return MIT_OK;
+  const long nblk = (rows + BWD_ROWS - 1) / BWD_ROWS;
+  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((2 * cols + 15) / 16)), dim3(256), 0, (hipStream_t)stream, nblk,
+                     cols, ws, dgamma, dbeta);
+  MIT_LAUNCH_CHECK("mit_layernorm_param_grads");
   return MIT_OK;
 }

@@ -152,6 +152,7 @@ class _Acts:
         self.count = f(1)
         self.loss_sum = f(1)
         self.loss = f(1)
+        self.row_loss = f(R)  # per-row CE losses (deterministic loss sum)
         # split-K scratch of the main stream: the d_model GEMMs (R x d outputs, 128 tiles at B = 64)
         # combine their K slices in-launch; weight-gradient / long-K GEMMs reduce in a second launch.
         # Zero-filled once: its first 4 KiB are tile counters the kernels leave at zero.
@@ -173,6 +174,9 @@ class _Acts:
             self.dmem = e(B * S, d)
             self.delta = f(B * H * T)
             self.ln_ws = f(native.layernorm_bwd_ws_floats(R, d))
+            # one column-partial buffer per LayerNorm: their dgamma/dbeta reductions run on the
+            # side stream, off the dX chain (run_backward)
+            self.ln_ws_side = [f(native.layernorm_bwd_ws_floats(R, d)) for _ in range(3 * L)]
             # the weight-gradient GEMMs run on a side stream (_SideStream) with their own scratch
             self.gemm_ws_side = torch.zeros(max(need, 4096) // 4 + 4, dtype=torch.float32, device=dev)
 
@@ -426,6 +430,18 @@ class TransformerDecoder:
             if side is not None:
                 side.guard(t)
 
+        def ln_bwd(l, k, dx, z, stt, dr, site):
+            """LayerNorm k (1..3) of layer l backward; dgamma/dbeta reduced on the side stream."""
+            gname, bname = f"layers.{l}.norm{k}.weight", f"layers.{l}.norm{k}.bias"
+            if side is None:
+                native.layernorm_bwd(dx, z, stt[0], stt[1], st.p(gname), dx, g(gname), g(bname), A.ln_ws, dr=dr,
+                                     drop_p=p, seed=seed, site=site)
+                return
+            ws_l = A.ln_ws_side[3 * l + k - 1]
+            native.layernorm_bwd(dx, z, stt[0], stt[1], st.p(gname), dx, None, None, ws_l, dr=dr, drop_p=p, seed=seed,
+                                 site=site)
+            side.run(lambda: native.layernorm_param_grads(R, d, ws_l, g(gname), g(bname)))
+
         def ready(first, last):
             if grads_ready is None:
                 return
@@ -446,9 +462,7 @@ class TransformerDecoder:
             xin = A.x0 if l == 0 else A.xs[l - 1][2]
             # LN3 -> dz3 (dx, in place) and d(ffn_out) (dy)
             guard(A.dy)
-            native.layernorm_bwd(A.dx, z[2], stt[2][0], stt[2][1], st.p(pre + "norm3.weight"), A.dx,
-                                 g(pre + "norm3.weight"), g(pre + "norm3.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
-                                 site=base + 5)
+            ln_bwd(l, 3, A.dx, z[2], stt[2], A.dy, base + 5)
             # FFN
             dW(A.dy, A.h[l], pre + "linear2.weight", pre + "linear2.bias", d, F, R, d, F)
             guard(A.dh)
@@ -459,9 +473,7 @@ class TransformerDecoder:
                         workspace=ws)
             # LN2
             guard(A.dy)
-            native.layernorm_bwd(A.dx, z[1], stt[1][0], stt[1][1], st.p(pre + "norm2.weight"), A.dx,
-                                 g(pre + "norm2.weight"), g(pre + "norm2.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
-                                 site=base + 3)
+            ln_bwd(l, 2, A.dx, z[1], stt[1], A.dy, base + 3)
             # cross-attention block
             dW(A.dy, A.oc[l], pre + "cross_out.weight", pre + "cross_out.bias", d, d, R, d, d)
             native.gemm(A.dy, w(pre + "cross_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)
@@ -478,9 +490,7 @@ class TransformerDecoder:
                         workspace=ws)
             # LN1
             guard(A.dy)
-            native.layernorm_bwd(A.dx, z[0], stt[0][0], stt[0][1], st.p(pre + "norm1.weight"), A.dx,
-                                 g(pre + "norm1.weight"), g(pre + "norm1.bias"), A.ln_ws, dr=A.dy, drop_p=p, seed=seed,
-                                 site=base + 1)
+            ln_bwd(l, 1, A.dx, z[0], stt[0], A.dy, base + 1)
             # self-attention block
             dW(A.dy, A.os[l], pre + "self_out.weight", pre + "self_out.bias", d, d, R, d, d)
             native.gemm(A.dy, w(pre + "self_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)

@@ -232,7 +232,7 @@ class ImageToTextModel:
         native.count_targets(targets, self.decoder_pad_idx, A.count)
         if dist is not None:
             dist.all_reduce_count(A.count)
-        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, True)
+        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, True, row_loss=A.row_loss)
         proj = (enc_rows, enc_ld, self.encoder_output_dim) if self.has_projection else None
         dec.run_backward(tokens, mem, mem_ld, S, A, self.seed_t, logits, proj_input=proj,
                          grads_ready=dist.grads_ready if dist is not None else None)
@@ -285,7 +285,7 @@ class ImageToTextModel:
         native.zero(A.count)
         native.zero(A.loss_sum)
         native.count_targets(targets, self.decoder_pad_idx, A.count)
-        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, False)
+        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, False, row_loss=A.row_loss)
         native.scalar_div(A.loss_sum, A.count, A.loss)
         return A.loss
 

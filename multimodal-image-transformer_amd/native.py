@@ -69,6 +69,7 @@ SIGNATURES = {
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
+    "mit_layernorm_param_grads": (I, [L, L, vp, vp, vp, vp]),
     "mit_attention_fwd": (I, [I, L, L, L, L, L, ctypes.POINTER(AttnArgs), vp]),
     "mit_attention_bwd": (I, [I, L, L, L, L, L, ctypes.POINTER(AttnArgs), ctypes.POINTER(AttnGrads), vp]),
     "mit_im2col": (I, [I, L, L, L, L, L, vp, vp, L, vp]),
@@ -76,7 +77,7 @@ SIGNATURES = {
     "mit_embed_fwd": (I, [I, L, L, L, vp, vp, Fl, vp, Fl, vp, U32, vp, vp]),
     "mit_embed_bwd": (I, [I, L, L, L, vp, vp, Fl, Fl, vp, U32, I, vp, vp]),
     "mit_count_targets": (I, [vp, L, I, vp, vp]),
-    "mit_cross_entropy": (I, [I, L, L, vp, L, vp, I, vp, vp, I, vp]),
+    "mit_cross_entropy": (I, [I, L, L, vp, L, vp, I, vp, vp, I, vp, vp]),
     "mit_colsum": (I, [I, L, L, vp, L, vp, I, vp, vp]),
     "mit_colsum_ws_floats": (L, [L, L]),
     "mit_grad_norm_ws_floats": (L, [L]),
@@ -245,11 +246,17 @@ def layernorm_bwd_ws_floats(rows, cols):
 
 
 def layernorm_bwd(dy, z, mean, rstd, gamma, dx, dgamma, dbeta, ws, *, dr=None, drop_p=0.0, seed=None, site=0):
+    """dgamma = dbeta = None: leave the column partials in ws for layernorm_param_grads."""
     cols = z.shape[-1]
     rows = z.numel() // cols
     _check(lib().mit_layernorm_bwd(dtype_code(z), rows, cols, ptr(dy), ptr(z), ptr(mean), ptr(rstd), ptr(gamma),
                                    ptr(dx), ptr(dr), drop_p, ptr(seed), site, ptr(dgamma), ptr(dbeta), ptr(ws),
                                    stream_ptr()), "mit_layernorm_bwd")
+
+
+def layernorm_param_grads(rows, cols, ws, dgamma, dbeta):
+    _check(lib().mit_layernorm_param_grads(rows, cols, ptr(ws), ptr(dgamma), ptr(dbeta), stream_ptr()),
+           "mit_layernorm_param_grads")
 
 
 def attn_args(q, q_row, q_batch, k, k_row, k_batch, v, v_row, v_batch, o, o_row, o_batch, *, lse=None,
@@ -301,12 +308,14 @@ def count_targets(targets, ignore_index, count):
            "mit_count_targets")
 
 
-def cross_entropy(logits, targets, ignore_index, count, loss_sum, want_grad, rows=None, V=None, ld=None):
-    """loss_sum += sum of -log p[target]; if want_grad, logits <- (softmax - onehot) / count (in place)."""
+def cross_entropy(logits, targets, ignore_index, count, loss_sum, want_grad, rows=None, V=None, ld=None,
+                  row_loss=None):
+    """loss_sum += sum of -log p[target]; if want_grad, logits <- (softmax - onehot) / count (in place).
+    row_loss: optional f32 [rows] scratch -> deterministic (row-ordered) loss sum."""
     V = V if V is not None else logits.shape[-1]
     rows = rows if rows is not None else targets.numel()
     _check(lib().mit_cross_entropy(dtype_code(logits), rows, V, ptr(logits), ld or V, ptr(targets), ignore_index,
-                                   ptr(count), ptr(loss_sum), 1 if want_grad else 0, stream_ptr()),
+                                   ptr(count), ptr(loss_sum), 1 if want_grad else 0, ptr(row_loss), stream_ptr()),
            "mit_cross_entropy")
 
 

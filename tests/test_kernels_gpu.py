@@ -149,6 +149,12 @@ def test_layernorm_fwd_bwd(dtype, cols):
     _close(dr, zr.grad, 3e-2 if dtype == torch.bfloat16 else 1e-4)
     _close(dg, gr.grad, 2e-2 if dtype == torch.bfloat16 else 1e-4)
     _close(db, br.grad, 2e-2 if dtype == torch.bfloat16 else 1e-4)
+    # deferred parameter reduction (partials left in ws, reduced later): identical results
+    dx2, dg2, db2 = torch.empty_like(x), torch.zeros(cols, device=dev()), torch.zeros(cols, device=dev())
+    ws2 = torch.empty_like(ws)
+    N.layernorm_bwd(dy, z, mean, rstd, g, dx2, None, None, ws2)
+    N.layernorm_param_grads(rows, cols, ws2, dg2, db2)
+    assert torch.equal(dx2, dx) and torch.equal(dg2, dg) and torch.equal(db2, db)
 
 
 def _attn_ref(q, k, v, causal, kpm, scale, drop=None):
@@ -321,3 +327,35 @@ def test_im2col_patch_embed(dtype):
     ref = F.conv2d(img.to(dtype).float(), w.to(dtype).float(), b, stride=P).flatten(2).transpose(1, 2)
     ref = torch.cat([cls.view(1, 1, E).expand(B, 1, E), ref], 1) + pos
     _close(h, ref, 2e-2 if dtype == torch.bfloat16 else 1e-4)
+
+
+@pytest.mark.parametrize("V", [1000, 10000, 10240, 12000])
+@pytest.mark.parametrize("want_grad", [True, False])
+def test_cross_entropy_row_kernel(V, want_grad):
+    """bf16 CE with the row_loss scratch: the register-resident one-wave-per-row kernel (V <= 10240)
+    or the generic one (V = 12000), against torch F.cross_entropy(ignore_index=0) in fp32; the loss
+    sum is row-ordered, so repeats are bit-identical."""
+    rows = 1003
+    g0 = torch.Generator().manual_seed(V)
+    logits = (3 * torch.randn(rows, V, generator=g0)).to(dev(), torch.bfloat16)
+    tgt = torch.randint(1, V, (rows,), generator=g0).to(dev())
+    tgt[::5] = 0
+    cnt = torch.zeros(1, device=dev())
+    N.count_targets(tgt, 0, cnt)
+    lr = logits.float().clone().requires_grad_(True)
+    ref = F.cross_entropy(lr, tgt, ignore_index=0)
+    ref.backward()
+    outs = []
+    for _ in range(2):
+        g = logits.clone()
+        ls = torch.zeros(1, device=dev())
+        N.cross_entropy(g, tgt, 0, cnt, ls, want_grad, row_loss=torch.empty(rows, device=dev()))
+        outs.append((g, ls))
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][0], outs[1][0])
+    g, ls = outs[0]
+    assert abs(ls.item() / cnt.item() - ref.item()) < 1e-4 * abs(ref.item()) + 1e-5
+    if want_grad:
+        _close(g, lr.grad, 1e-2)
+        assert torch.count_nonzero(g[::5]).item() == 0  # ignored rows
+    else:
+        assert torch.equal(g, logits)
