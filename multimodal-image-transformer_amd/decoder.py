@@ -191,23 +191,26 @@ class _SideStream:
 
     def __init__(self, device):
         self.stream = torch.cuda.Stream(device=device)
-        self.pending = {}
+        self.ptr = self.stream.cuda_stream
+        self.events = native.HipEvents(64)  # recorded on the main stream (side waits for main)
+        self.side_events = native.HipEvents(128)  # recorded on the side stream only: a recycled slot
+        self.pending = {}                         # re-recorded later on the SAME stream stays a safe wait
 
     def run(self, fn, reads=()):
-        main = torch.cuda.current_stream()
-        self.stream.wait_stream(main)
-        with torch.cuda.stream(self.stream):
+        """fn issues native launches only (routed by native.on_stream, no torch stream switch)."""
+        self.events.wait_stream(self.ptr, native.stream_ptr())
+        with native.on_stream(self.ptr):
             fn()
-        ev = torch.cuda.Event()
-        ev.record(self.stream)
-        for t in reads:
-            self.pending[t.data_ptr()] = ev
+        if reads:
+            ev = self.side_events.record(self.ptr)
+            for t in reads:
+                self.pending[t.data_ptr()] = ev
 
     def guard(self, t):
         """Before the main stream writes t: wait for the side-stream GEMM still reading it."""
         ev = self.pending.pop(t.data_ptr(), None)
         if ev is not None:
-            torch.cuda.current_stream().wait_event(ev)
+            native.HipEvents.wait(native.stream_ptr(), ev)
 
     def under(self, fn):
         """Run fn (e.g. a DP gradient-bucket all-reduce) on the side stream after everything issued

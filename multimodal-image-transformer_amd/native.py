@@ -134,8 +134,72 @@ def ptr(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+_stream_override = None
+
+
 def stream_ptr():
-    return torch.cuda.current_stream().cuda_stream
+    """The stream native launches go to: the innermost on_stream() override, else torch's current
+    stream (raw lookup: torch.cuda.current_stream() costs ~8 us of Python per call)."""
+    if _stream_override is not None:
+        return _stream_override
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
+
+
+class on_stream:
+    """Route native launches (only) to the raw HIP stream `ptr` inside the block. torch ops keep
+    torch's current stream: use torch.cuda.stream() around code that mixes in torch ops."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __enter__(self):
+        global _stream_override
+        self.prev, _stream_override = _stream_override, self.ptr
+
+    def __exit__(self, *exc):
+        global _stream_override
+        _stream_override = self.prev
+
+
+class HipEvents:
+    """Timing-free HIP events from a recycled pool, recorded / waited on raw stream pointers
+    (cross-stream edges of the step without torch.cuda.Event's Python overhead)."""
+    _hip = None
+    DISABLE_TIMING = 0x2
+
+    def __init__(self, n=64):
+        if HipEvents._hip is None:
+            h = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded
+            h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
+            h.hipEventRecord.argtypes = [vp, vp]
+            h.hipStreamWaitEvent.argtypes = [vp, vp, ctypes.c_uint]
+            h.hipEventDestroy.argtypes = [vp]
+            HipEvents._hip = h
+        self.pool = []
+        for _ in range(n):
+            ev = vp()
+            if HipEvents._hip.hipEventCreateWithFlags(ctypes.byref(ev), self.DISABLE_TIMING) != 0:
+                raise NativeError("hipEventCreateWithFlags failed")
+            self.pool.append(ev)
+        self.i = 0
+
+    def record(self, stream):
+        """Record the next pool event on `stream`; returns it. A pool slot is reused after len(pool)
+        records: callers wait on an event well before that (one step issues < 64)."""
+        ev = self.pool[self.i]
+        self.i = (self.i + 1) % len(self.pool)
+        if HipEvents._hip.hipEventRecord(ev, stream) != 0:
+            raise NativeError("hipEventRecord failed")
+        return ev
+
+    @staticmethod
+    def wait(stream, ev):
+        if HipEvents._hip.hipStreamWaitEvent(stream, ev, 0) != 0:
+            raise NativeError("hipStreamWaitEvent failed")
+
+    def wait_stream(self, stream, other):
+        """stream waits for everything issued so far on other."""
+        self.wait(stream, self.record(other))
 
 
 def dtype_code(t: torch.Tensor) -> int:

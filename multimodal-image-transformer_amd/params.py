@@ -39,21 +39,24 @@ class FlatParams:
         self.exp_avg = None
         self.exp_avg_sq = None
 
-    # views ------------------------------------------------------------------------------------
-    def _view(self, buf, name):
-        shape, off, n = self.index[name]
-        return buf[off:off + n].view(shape)
+    # views (cached: the buffers are allocated once and only ever updated in place) -------------
+    def _view(self, buf, name, cache):
+        v = cache.get(name)
+        if v is None:
+            shape, off, n = self.index[name]
+            v = cache[name] = buf[off:off + n].view(shape)
+        return v
 
     def p(self, name):
         """f32 master view."""
-        return self._view(self.master, name)
+        return self._view(self.master, name, self.__dict__.setdefault("_pv", {}))
 
     def w(self, name):
         """compute-dtype view (what kernels read)."""
-        return self._view(self.shadow, name)
+        return self._view(self.shadow, name, self.__dict__.setdefault("_wv", {}))
 
     def g(self, name):
-        return self._view(self.grad, name)
+        return self._view(self.grad, name, self.__dict__.setdefault("_gv", {}))
 
     def span(self, first: str, last: str):
         """[start, end) element range covering entries first..last (inclusive, layout order)."""
