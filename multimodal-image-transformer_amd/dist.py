@@ -33,8 +33,8 @@ def init_from_env(backend: str = None):
         return 0, 1
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # MIT_DIST_BACKEND=gloo: rehearse N ranks on one GPU (tools/gpu_dp_smoke.sh)
+        backend = os.environ.get("MIT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
         dist.init_process_group(backend, device_id=torch.device("cuda", local))

@@ -1,0 +1,7 @@
+# The bench's N>1 code path (DataParallel buckets on the side stream, encoder prefetch, loss
+# all-reduce) on ONE GPU: 2 ranks over gloo sharing cuda:0 (RCCL needs one GPU per rank).
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+MIT_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --no-roofline \
+  > gpurun_out/dp2_gloo.json 2> gpurun_out/dp2_gloo.err
