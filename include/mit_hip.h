@@ -259,6 +259,16 @@ int mit_cast_f32(int dtype, long n, const float* src, void* dst, void* stream);
 int mit_zero(void* p, long bytes, void* stream);
 int mit_dropout_mask(long n, float p, const uint64_t* seed, uint32_t site, float* out, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Data path: rescale + normalise + HWC->CHW of a batch of uint8 RGB images
+ * already resized / centre-cropped on the host (PIL, as the reference's HF processors do:
+ * dataset.py:135, model.py:192; ViT mean = std = 0.5, CLIP OPENAI mean/std):
+ *   dst[b, c, y, x] = ((float)src[b, y, x, c] / 255 - mean3[c]) / std3[c]   (f32, bit-identical
+ *   to the processor's numpy pixel_values). src [B,H,W,3] uint8 (4-B aligned), dst [B,3,H,W] f32
+ *   (16-B aligned); H*W % 4 == 0. mean3/std3: HOST arrays of 3 floats. */
+int mit_image_normalize(long B, long H, long W, const uint8_t* src, float* dst, const float* mean3, const float* std3,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

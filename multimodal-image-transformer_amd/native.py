@@ -91,6 +91,7 @@ SIGNATURES = {
     "mit_attention_decode": (I, [I, L, L, vp, L, vp, L, L, vp, L, L, vp, L, L, vp, vp, L, I, Fl, vp]),
     "mit_kv_store": (I, [I, L, L, vp, L, vp, L, L, vp, vp]),
     "mit_embed_decode": (I, [I, L, L, vp, L, vp, vp, Fl, vp, vp, vp]),
+    "mit_image_normalize": (I, [L, L, L, vp, vp, ctypes.POINTER(Fl), ctypes.POINTER(Fl), vp]),
     "mit_greedy_pick": (I, [L, L, vp, L, vp, L, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp]),
 }
 
@@ -451,3 +452,13 @@ def greedy_pick(logits, ids, pos, end_id, pad_id, finished, n_finished):
     B, V = logits.shape
     _check(lib().mit_greedy_pick(B, V, ptr(logits), logits.stride(0), ptr(ids), ids.shape[1], ptr(pos), int(end_id),
                                  int(pad_id), ptr(finished), ptr(n_finished), stream_ptr()), "mit_greedy_pick")
+
+
+def image_normalize(src_u8, dst, mean, std):
+    """dst [B,3,H,W] f32 <- (src [B,H,W,3] uint8 / 255 - mean) / std (mit_image_normalize)."""
+    B, H, W, C = src_u8.shape
+    if C != 3 or src_u8.dtype != torch.uint8 or dst.dtype != torch.float32:
+        raise NativeError("image_normalize: src uint8 [B,H,W,3], dst f32 [B,3,H,W]")
+    m = (Fl * 3)(*[float(x) for x in mean])
+    s = (Fl * 3)(*[float(x) for x in std])
+    _check(lib().mit_image_normalize(B, H, W, ptr(src_u8), ptr(dst), m, s, stream_ptr()), "mit_image_normalize")

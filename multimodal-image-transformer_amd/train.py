@@ -22,6 +22,7 @@ import time
 import torch
 
 import config
+import data
 import optim
 from model import ImageToTextModel
 
@@ -37,12 +38,20 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
     total = torch.zeros(1, dtype=torch.float32, device=model.device)
     n = 0
 
+    pre = None
+
     def staged(it):
         # images go to the device once, so the next step can consume the encoder output that
-        # model.prefetch_encoder computed for this very tensor one step earlier
+        # model.prefetch_encoder computed for this very tensor one step earlier; uint8 batches
+        # (data.collate_fn) are normalised there by one kernel (data.to_device)
+        nonlocal pre
         for b in it:
             b = dict(b)
-            b["images"] = b["images"].to(model.device, non_blocking=True)
+            if b["images"].dtype == torch.uint8:
+                pre = pre or data.ImagePreprocessor.for_encoder(device=model.device)
+                b["images"] = pre.normalize(b["images"])
+            else:
+                b["images"] = b["images"].to(model.device, non_blocking=True)
             yield b
 
     it = staged(dataloader)
@@ -76,8 +85,13 @@ def evaluate(model, dataloader, criterion, device):
     model.eval()
     total = torch.zeros(1, dtype=torch.float32, device=model.device)
     n = 0
+    pre = None
     for batch in dataloader:
-        total += model.eval_loss(batch["images"], batch["decoder_input_tokens"], batch["target_tokens"])
+        images = batch["images"]
+        if images.dtype == torch.uint8:  # data.collate_fn batches: normalised on the GPU
+            pre = pre or data.ImagePreprocessor.for_encoder(device=model.device)
+            images = pre.normalize(images)
+        total += model.eval_loss(images, batch["decoder_input_tokens"], batch["target_tokens"])
         n += 1
     model.train()
     return (total / max(n, 1)).item()
