@@ -831,6 +831,189 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_mfma(long H, long Lq, long L
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16 MFMA backward, head-resident and fused (the decoder: Lq <= 64 queries, Lk <= 256 keys).
+// One 8-wave workgroup per (b, h). The split dQ / dKV kernels above each walk a dependent chain
+// of global round trips per 64-row tile (a 63 x 197 head is 55 us for two launches at under one
+// resident wave per SIMD); here every operand of the head -- K, Q, dO into LDS; each wave's V
+// strips, O / lse for delta into registers -- is requested in ONE batch of loads, and then:
+//   phase A (waves over 16-key strips, key on the lane): S = Q K^T, dP = dO V^T for all 64 queries
+//     -> P (mask, dropout), dS = P o (dP o M - delta); dV += (P o M)^T dO, dK += dS^T Q (A by
+//     transposed LDS reads), written straight out; dS^T (bf16) kept in LDS as a [key][64 query]
+//     tile in the K-tile swizzle (four 8-byte stores per strip and lane).
+//   phase B (waves over 16 queries x 32 head dims): dQ^T = K^T dS^T, both operands by transposed
+//     LDS reads of the K and dS^T tiles (the same permuted k order on both sides).
+// The dropout mask and exp are evaluated once per element (the split kernels evaluate both twice).
+// LDS: (2 * Lk + 128) rows x 128 B <= 80 KiB, so two workgroups share a CU (<= 128 VGPRs).
+// ------------------------------------------------------------------------------------------------
+constexpr int HB_MAXK = 256;  // keys per head
+constexpr int HB_NT = 512;    // 8 waves
+constexpr int HB_SPW = HB_MAXK / 16 / 8;  // key strips per wave (<= 2)
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_head(long H, long Lq, long Lk, AttnK a, AttnG gr, AttnBwdBytes nb_,
+                                                        int lkp) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* Ks = lds;                // [lkp][64] bf16
+  char* St = Ks + lkp * 128;     // dS^T [lkp][64] bf16
+  char* Qs = St + lkp * 128;     // [64][64]
+  char* Ds = Qs + 64 * 128;      // dO [64][64]
+  float* Ls = (float*)(Ds + 64 * 128);
+  float* Dl = Ls + 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const long h = blockIdx.x, b = blockIdx.y, bh = b * H + h;
+  const bf16* Qb = (const bf16*)a.q + b * a.q_batch + h * D;
+  const bf16* Kb = (const bf16*)a.k + b * a.k_batch + h * D;
+  const bf16* Vb = (const bf16*)a.v + b * a.v_batch + h * D;
+  const bf16* dOb = (const bf16*)gr.dout + b * gr.do_batch + h * D;
+  const bf16* Ob = (const bf16*)a.o + b * a.o_batch + h * D;
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, nb_.v, 0x00020000);
+  // ---- one batch of loads ----
+  bf16x8 vf[HB_SPW][2];  // B operand of dP = dO V^T for this wave's strips (key on the lane)
+#pragma unroll
+  for (int si = 0; si < HB_SPW; ++si)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const long kl = (w + 8 * si) * 16 + (lane & 15);
+      const bool ok = kl < Lk;
+      vf[si][kk] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                      rv, (int)(ok ? (uint32_t)((kl * a.v_row + kk * 32 + g * 8) * 2) : A_OOB), 0, 0));
+    }
+  {
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, nb_.k, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)Qb, (short)0, nb_.q, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dOb, (short)0, nb_.dO, 0x00020000);
+    u32x4 kr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + HB_NT * i, r = c >> 3, ch = c & 7;
+      const bool ok = r < Lk && c < lkp * 8;
+      kr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rk, (int)(ok ? (uint32_t)((r * a.k_row + ch * 8) * 2) : A_OOB), 0, 0));
+    }
+    const int r = tid >> 3, ch = tid & 7;  // 64 rows x 8 chunks = 512 threads
+    const bool qok = r < Lq;
+    const u32x4 qr = __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, (int)(qok ? (uint32_t)((r * a.q_row + ch * 8) * 2) : A_OOB), 0, 0));
+    const u32x4 dr = __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, (int)(qok ? (uint32_t)((r * gr.do_row + ch * 8) * 2) : A_OOB), 0, 0));
+    bf16x8 ov = {};
+    if (qok) ov = *(const bf16x8*)(Ob + r * a.o_row + ch * 8);
+    const float l = (qok && ch == 0) ? a.lse[bh * Lq + r] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + HB_NT * i;
+      if (c < lkp * 8) *(u32x4*)(Ks + koff_k(c >> 3, c & 7)) = kr[i];
+    }
+    *(u32x4*)(Qs + koff_k(r, ch)) = qr;
+    *(u32x4*)(Ds + koff_k(r, ch)) = dr;
+    // delta = rowsum(dO o O): 8 lanes per query
+    const bf16x8 dv8 = __builtin_bit_cast(bf16x8, dr);
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl += (float)dv8[j] * (float)ov[j];
+    dl += __shfl_xor(dl, 1, 64);
+    dl += __shfl_xor(dl, 2, 64);
+    dl += __shfl_xor(dl, 4, 64);
+    if (ch == 0) {
+      Ls[r] = l * 1.4426950408889634f;
+      Dl[r] = dl;
+      if (qok) gr.delta[bh * Lq + r] = dl;
+    }
+  }
+  __syncthreads();
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const uint64_t key = a.dropout ? site_key(a.seed, a.site) : 0ull;
+  const int64_t* tok = a.tok ? a.tok + b * a.tok_batch : nullptr;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  // ---- phase A: key strips ----
+#pragma unroll
+  for (int si = 0; si < HB_SPW; ++si) {
+    const int ks = w + 8 * si;
+    if (ks * 16 >= lkp) break;
+    const int kloc = ks * 16 + (lane & 15);
+    const long kl = kloc;
+    const bool klive = kl < Lk;
+    const bool kpad = klive && tok && tok[kl] == a.pad;
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) s[nb] = dp[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 kf = lds_row_frag(Ks, kloc, kk * 4 + g);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        s[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_row_frag(Qs, nb * 16 + (lane & 15), kk * 4 + g), kf, s[nb],
+                                                        0, 0, 0);
+        dp[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_row_frag(Ds, nb * 16 + (lane & 15), kk * 4 + g), vf[si][kk],
+                                                         dp[nb], 0, 0, 0);
+      }
+    }
+    bf16x4 bp4[4], bs4[4];  // (P o M) and dS, 4 consecutive queries (t) per 16-query block nb
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int qq = nb * 16 + g * 4 + t;
+        const bool msk = !klive || kpad || qq >= Lq || (a.causal && kl > qq);
+        const float p = msk ? 0.f : exp2f(s[nb][t] * sl2 - Ls[qq]);
+        const float mul =
+            a.dropout ? drop_mul(key, ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qq) * (uint64_t)Lk + kl, a.thresh, a.dscale)
+                      : 1.f;
+        bp4[nb][t] = (bf16)(p * mul);
+        bs4[nb][t] = (bf16)(p * (dp[nb][t] * mul - Dl[qq]));
+      }
+      // dS^T row kloc, queries nb*16+4g .. +4: 8 bytes in the K-tile swizzle
+      *(bf16x4*)(St + koff_k(kloc, nb * 2 + (g >> 1)) + (g & 1) * 8) = bs4[nb];
+    }
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 bp = {bp4[2 * kk][0], bp4[2 * kk][1], bp4[2 * kk][2], bp4[2 * kk][3],
+                         bp4[2 * kk + 1][0], bp4[2 * kk + 1][1], bp4[2 * kk + 1][2], bp4[2 * kk + 1][3]};
+      const bf16x8 bs = {bs4[2 * kk][0], bs4[2 * kk][1], bs4[2 * kk][2], bs4[2 * kk][3],
+                         bs4[2 * kk + 1][0], bs4[2 * kk + 1][1], bs4[2 * kk + 1][2], bs4[2 * kk + 1][3]};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dv[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_tr_frag(Ds, kk * 32, i * 16, lane), bp, dv[i], 0, 0, 0);
+        dk[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_tr_frag(Qs, kk * 32, i * 16, lane), bs, dk[i], 0, 0, 0);
+      }
+    }
+    if (klive) {
+      bf16* DK = (bf16*)gr.dk + b * gr.dk_batch + kl * gr.dk_row + h * D;
+      bf16* DV = (bf16*)gr.dv + b * gr.dv_batch + kl * gr.dv_row + h * D;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        *(bf16x4*)(DK + i * 16 + g * 4) = bf16x4{(bf16)(dk[i][0] * a.scale), (bf16)(dk[i][1] * a.scale),
+                                                 (bf16)(dk[i][2] * a.scale), (bf16)(dk[i][3] * a.scale)};
+        *(bf16x4*)(DV + i * 16 + g * 4) = bf16x4{(bf16)dv[i][0], (bf16)dv[i][1], (bf16)dv[i][2], (bf16)dv[i][3]};
+      }
+    }
+  }
+  __syncthreads();
+  // ---- phase B: dQ^T (16 head dims x 16 queries tiles) = K^T dS^T; wave = (query strip, dim half) ----
+  {
+    const int qs = w & 3, dh = w >> 2;
+    const int qq = qs * 16 + (lane & 15);
+    f32x4 dq[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int k0 = 0; k0 < lkp; k0 += 32) {
+      const bf16x8 bsf = lds_tr_frag(St, k0, qs * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        dq[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds_tr_frag(Ks, k0, dh * 32 + i * 16, lane), bsf, dq[i], 0, 0, 0);
+    }
+    if (qq < Lq) {
+      bf16* DQ = (bf16*)gr.dq + b * gr.dq_batch + (long)qq * gr.dq_row + h * D + dh * 32;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        *(bf16x4*)(DQ + i * 16 + g * 4) = bf16x4{(bf16)(dq[i][0] * a.scale), (bf16)(dq[i][1] * a.scale),
+                                                 (bf16)(dq[i][2] * a.scale), (bf16)(dq[i][3] * a.scale)};
+    }
+  }
+}
+
 AttnK make_k(const mit_attn_args* x) {
   AttnK a;
   a.q = x->q; a.q_row = x->q_row; a.q_batch = x->q_batch;
@@ -933,8 +1116,21 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
     nb.k = (int)kb;
     nb.v = (int)vb;
     nb.dO = (int)db;
-    hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 0, s, H, Lq, Lk, a, g, nb);
-    hipLaunchKernelGGL(attn_bwd_dkv_mfma, gk, dim3(256), 0, s, H, Lq, Lk, a, g, nb);
+    static const int head_ok = getenv("MIT_ATTN_HEAD") ? atoi(getenv("MIT_ATTN_HEAD")) : 1;
+    if (head_ok && Lq <= 64 && Lk <= HB_MAXK && H <= 65535 && B <= 65535 && x->o_row % 8 == 0) {
+      const int lkp = (int)((Lk + 31) / 32 * 32);
+      const int lds = 2 * lkp * 128 + 2 * 64 * 128 + 2 * 64 * 4;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)attn_bwd_head, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  2 * HB_MAXK * 128 + 2 * 64 * 128 + 2 * 64 * 4);
+        attr = true;
+      }
+      hipLaunchKernelGGL(attn_bwd_head, dim3((unsigned)H, (unsigned)B), dim3(HB_NT), lds, s, H, Lq, Lk, a, g, nb, lkp);
+    } else {
+      hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 0, s, H, Lq, Lk, a, g, nb);
+      hipLaunchKernelGGL(attn_bwd_dkv_mfma, gk, dim3(256), 0, s, H, Lq, Lk, a, g, nb);
+    }
   } else if (dtype == MIT_BF16) {
     hipLaunchKernelGGL(attn_bwd_dq_simple<bf16>, gq, dim3(64), 0, s, H, Lq, Lk, a, g);
     hipLaunchKernelGGL(attn_bwd_dkv_simple<bf16>, gk, dim3(64), 0, s, H, Lq, Lk, a, g);

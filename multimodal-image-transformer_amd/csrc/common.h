@@ -23,18 +23,24 @@ template <> __device__ __forceinline__ float from_f<float>(float x) { return x; 
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
 
 // ---------------------------------------------------------------------------------------------
-// Counter-based dropout RNG: keep(i) = mix64(seed ^ site, i) >= p * 2^32. Stateless, so the
+// Counter-based dropout RNG: keep(i) = mix(seed ^ site, i) >= p * 2^32. Stateless, so the
 // backward regenerates the forward's mask from (seed, site, element index) without storing it.
 // The seed lives in device memory so a captured hipGraph replays with a fresh seed per step.
 // ---------------------------------------------------------------------------------------------
+// 32-bit "lowbias32" permutation (2 multiplies): the backward regenerates every mask element of
+// the attention / FFN / residual dropouts, so the hash is VALU work on the critical kernels (a
+// 64-bit splitmix finaliser cost ~3x the instructions: ~9 32-bit multiplies per element)
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t mix_u32(uint64_t key, uint64_t idx) {
-  uint64_t x = key ^ (idx * 0x9E3779B97F4A7C15ull);
-  x ^= x >> 31;
-  x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 29;
-  x *= 0x94D049BB133111EBull;
-  x ^= x >> 32;
-  return (uint32_t)x;
+  uint32_t x = lowbias32((uint32_t)idx ^ (uint32_t)key);
+  return lowbias32(x ^ (uint32_t)(idx >> 32) ^ (uint32_t)(key >> 32));
 }
 __device__ __forceinline__ uint64_t site_key(const uint64_t* seed, uint32_t site) {
   return (seed ? *seed : 0ull) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(site + 1));
