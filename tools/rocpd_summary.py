@@ -45,7 +45,30 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--command", default="")
+    ap.add_argument("--trace-csv", default=None, help="kernel trace CSV of the same run: the GEMM launches of "
+                    "bench.py's roofline replay (after the last AdamW) averaged per (kernel, a_layout, b_layout)")
+    ap.add_argument("--bench-json", default=None, help="bench.py output line to cross-check")
     a = ap.parse_args()
+    if a.trace_csv:
+        import collections
+        import csv
+        rows = sorted(csv.DictReader(open(a.trace_csv)), key=lambda r: int(r["Start_Timestamp"]))
+        last = max(i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"])
+        d = collections.defaultdict(list)
+        for r in rows[last + 1:]:
+            m = re.search(r"(gemm256_kernel|gemm_bf16_kernel)<(\d), (\d)", r["Kernel_Name"])
+            if m:
+                d[f"{m.group(1)}<{m.group(2)},{m.group(3)}>"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        chk = {"source": "rocprofv3 --kernel-trace of bench.py: the roofline replay launches (after the last AdamW)",
+               "avg_us_trace": {k: round(sum(v) / len(v) / 1e3, 2) for k, v in sorted(d.items())},
+               "launches_trace": {k: len(v) for k, v in sorted(d.items())}}
+        if a.bench_json:
+            line = [x for x in open(a.bench_json) if x.startswith("{")][-1]
+            rf = json.loads(line).get("roofline", {})
+            chk["bench_roofline"] = {"kernel": rf.get("kernel"), "avg_launch_us": rf.get("avg_launch_us")}
+        with open(a.out + "_roofline_check.json", "w") as f:
+            json.dump(chk, f, indent=1)
+        print(json.dumps(chk))
     ks = kernel_stats(a.trace)
     fe, wr = pmc(a.fetch, "FETCH_SIZE"), pmc(a.write, "WRITE_SIZE")
     out = {"command": a.command,
