@@ -108,6 +108,23 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return x * (x >= 0.0f ? 1.0f - h : h);
 }
 
+// gelu_fast on two values with packed FP32 math (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of
+// the polynomial per instruction); the rcp / exp stay scalar. Same operations, same results.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
+  const f32x2 a = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f32x2 d = __builtin_elementwise_fma(f32x2{0.3275911f, 0.3275911f}, a, f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 p = __builtin_elementwise_fma(f32x2{1.061405429f, 1.061405429f}, t, f32x2{-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, f32x2{1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.254829592f, 0.254829592f});
+  const f32x2 na2 = -a * a;
+  const f32x2 e = {__expf(na2[0]), __expf(na2[1])};
+  const f32x2 h = 0.5f * p * t * e;
+  return x * f32x2{x[0] >= 0.0f ? 1.0f - h[0] : h[0], x[1] >= 0.0f ? 1.0f - h[1] : h[1]};
+}
+
 // error plumbing shared by every C-ABI entry point (capi.cpp)
 int mit_set_error(const char* fmt, ...);
 #define MIT_CHECK_ARG(cond, ...)          \

@@ -93,7 +93,14 @@ __device__ __forceinline__ void epi8(const Epi& e, void* C, long ldc, long N, lo
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] = v[k] * e.alpha + b[k];
-  if (ACT != MIT_ACT_NONE) {
+  if (ACT == MIT_ACT_GELU) {  // packed pairs (v_pk_* FP32): the fc1 + GELU epilogue is VALU-bound
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+      const f32x2 r = gelu_fast2(f32x2{v[k], v[k + 1]});
+      v[k] = r[0];
+      v[k + 1] = r[1];
+    }
+  } else if (ACT != MIT_ACT_NONE) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = act_apply<ACT, true>(e.act, v[k]);
   }

@@ -189,8 +189,8 @@ class _SideStream:
     side's last reader of a gradient buffer before overwriting it (guard); join() at the end. All
     edges are HIP events, so the step still captures into ONE hipGraph (as parallel branches)."""
 
-    def __init__(self, device):
-        self.stream = torch.cuda.Stream(device=device)
+    def __init__(self, device, priority: int = 0):
+        self.stream = torch.cuda.Stream(device=device, priority=priority)
         self.ptr = self.stream.cuda_stream
         self.events = native.HipEvents(64)  # recorded on the main stream (side waits for main)
         self.side_events = native.HipEvents(128)  # recorded on the side stream only: a recycled slot
@@ -288,6 +288,7 @@ class TransformerDecoder:
         # weight-gradient GEMMs on a second stream (MIT_DW_SIDE_STREAM=0 disables, for A/B)
         self.dw_side_stream = os.environ.get("MIT_DW_SIDE_STREAM", "1") != "0"
         self._side = None
+        self.side_priority = 0  # set by ImageToTextModel.train_step (high priority beside the encoder)
         if self._own_store:
             self.init_weights(0)
 
@@ -334,7 +335,7 @@ class TransformerDecoder:
 
     def _side_stream(self) -> "_SideStream":
         if self._side is None:
-            self._side = _SideStream(self.device)
+            self._side = _SideStream(self.device, self.side_priority)
         return self._side
 
     # --- forward -----------------------------------------------------------------------------
