@@ -171,20 +171,36 @@ def pmc_traffic(kernel_prefix):
     return (round(tot / n), f"profiles/{PMC_SUMMARY}") if n else (None, None)
 
 
+# Train workloads: BASELINE.json configs[1] (the metric's config, the default) and the single-GPU
+# shares of configs[2] / configs[3] (CLIP encoders; cfg3 = 64 of its global 512 pairs per GPU).
+# (encoder name, decoder d, heads, layers, ff, workload label)
+WORKLOADS = {
+    "train": ("google/vit-base-patch16-224-in21k", 512, 8, 6, 2048,
+              "configs[1]: 6L d512 decoder + ViT-B/16 (197 patches), batch 64/GPU, seq_len 64"),
+    "clip336": ("openai/clip-vit-large-patch14-336", 512, 8, 6, 2048,
+                "configs[2]: 6L d512 decoder + CLIP ViT-L/14@336 (577 patches), batch 64/GPU, seq_len 64"),
+    "cfg3": ("openai/clip-vit-large-patch14", 768, 12, 12, 3072,
+             "configs[3]: 12L d768 decoder + CLIP ViT-L/14 (257 patches), batch 64/GPU (global 512 at 8 GPUs), "
+             "seq_len 64"),
+}
+
+
 def build(args, rank):
     import config
     from model import ImageToTextModel
     import optim
     config.MEMORY_MODE = args.memory_mode
-    m = ImageToTextModel(args.vocab, 512, 8, 6, 2048, 100, 0.1, 0, memory_mode=args.memory_mode, dtype=args.dtype,
+    enc_name, d, heads, layers, ff, _ = WORKLOADS.get(args.workload, WORKLOADS["train"])
+    config.ENCODER_MODEL_NAME = enc_name
+    m = ImageToTextModel(args.vocab, d, heads, layers, ff, 100, 0.1, 0, memory_mode=args.memory_mode, dtype=args.dtype,
                          seed=42)
     opt = optim.AdamW(m.store, lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-5)
     return m, opt
 
 
-def synthetic_batch(B, seq_len, vocab, device, seed):
+def synthetic_batch(B, seq_len, vocab, device, seed, image=224):
     g = torch.Generator().manual_seed(seed)
-    images = torch.randn(B, 3, 224, 224, generator=g).to(device)
+    images = torch.randn(B, 3, image, image, generator=g).to(device)
     cap = torch.randint(4, vocab, (B, seq_len), generator=g)
     cap[:, 0] = 2
     return images, cap[:, :-1].contiguous().to(device), cap[:, 1:].contiguous().to(device)
@@ -279,9 +295,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="(default; kept for older scripts)")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="run the frozen encoder inside each step instead of one step ahead on a second stream")
-    ap.add_argument("--workload", default="train", choices=["train", "decode"],
-                    help="train: the BASELINE metric (default). decode: configs[4], batched greedy captioning "
-                         "(KV cache, hipGraph-replayed token step)")
+    ap.add_argument("--workload", default="train", choices=["train", "clip336", "cfg3", "decode"],
+                    help="train: the BASELINE metric (default, configs[1]). clip336 / cfg3: the one-GPU share of "
+                         "configs[2] / configs[3] (same step, CLIP-L encoders). decode: configs[4], batched greedy "
+                         "captioning (KV cache, hipGraph-replayed token step)")
     ap.add_argument("--decode-batch", type=int, default=256)
     ap.add_argument("--max-len", type=int, default=100, help="decode: ids per caption (config.MAX_SEQ_LEN)")
     args = ap.parse_args()
@@ -297,7 +314,7 @@ def main():
     model, opt = build(args, rank)
     dp = DataParallel(model, overlap=not args.no_overlap) if world > 1 else None
     model.train()
-    images, di, tg = synthetic_batch(args.batch, args.seq_len, args.vocab, dev, 1000 + rank)
+    images, di, tg = synthetic_batch(args.batch, args.seq_len, args.vocab, dev, 1000 + rank, model.encoder.image)
 
     prefetch = not args.no_prefetch
 
@@ -342,11 +359,14 @@ def main():
     value = pairs / elapsed
     flops_pair = model.flops_per_pair(args.seq_len - 1)
     out = {
-        "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC if args.workload == "train" else METRIC.replace(
+            "6L/d512 decoder + ViT-B/16, 1/2/4/8 GPU", WORKLOADS[args.workload][5].split(": ")[1].split(",")[0]),
+        "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.dtype == "bf16" else "f32",
-        "data": "synthetic (randn 224x224 images, uniform caption ids; random-init weights)",
-        "config": {"workload": "configs[1]: 6L d512 decoder + ViT-B/16 (197 patches), batch 64/GPU, seq_len 64",
+        "data": f"synthetic (randn {model.encoder.image}x{model.encoder.image} images, uniform caption ids; "
+                "random-init weights)",
+        "config": {"workload": WORKLOADS[args.workload][5],
                    "global_batch": args.batch * world, "seq_len": args.seq_len, "vocab": args.vocab,
                    "memory_mode": args.memory_mode, "parallelism": f"dp{world}",
                    "gflop_per_pair": round(flops_pair / 1e9, 3)},
@@ -377,7 +397,8 @@ def main():
         key = max(agg, key=lambda k: agg[k][0])
         t, fl, n, nb = agg[key]
         ach = fl / t / 1e12
-        traffic, src = pmc_traffic(f"{key[0]}<{key[1]}, {key[2]},")
+        # the committed PMC summary was collected on configs[1]; other workloads report no traffic
+        traffic, src = (pmc_traffic(f"{key[0]}<{key[1]}, {key[2]},") if args.workload == "train" else (None, None))
         out["roofline"] = {"bound": "mfma", "kernel": names(key), "achieved": round(ach, 1),
                            "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
                            "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
@@ -389,7 +410,7 @@ def main():
         out["gemm_breakdown"] = {names(k): {"tflops": round(v[1] / v[0] / 1e12, 1),
                                                         "ms_per_step": round(1e3 * v[0] * inplace[k][2] / v[2] / min(args.steps, 5), 3)}
                                  for k, v in agg.items()}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "train":
         out["cpu_baseline"] = cpu_baseline(model, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
