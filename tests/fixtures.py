@@ -13,7 +13,8 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 sys.path.insert(0, GOLDEN)
 import procedural as P  # noqa: E402
 
-CASES = ["tiny_vit_cls", "tiny_vit_patches", "tiny_clip336_patches", "tiny_clip336_cls", "cfg1_b2_patches"]
+CASES = ["tiny_vit_cls", "tiny_vit_patches", "tiny_clip336_patches", "tiny_clip336_cls", "cfg1_b2_patches",
+         "cfg3_b2_patches"]
 
 
 @lru_cache(maxsize=None)
@@ -109,6 +110,8 @@ def compare_stat(prefix, name, t, tensors, meta, rtol, atol, scale_tol=0.0, outl
             m = gm if m is None else (m & gm)
         if m is not None:
             got, ref = got.flatten()[m], ref.flatten()[m]
+        if got.numel() == 0:  # every element excluded above (degenerate / below the pinning floor)
+            return 0.0
         if outlier_frac:
             _assert_close_outliers(got.flatten(), ref.flatten(), rtol, atol, outlier_frac, 10 * atol, f"{prefix} {name}")
         else:

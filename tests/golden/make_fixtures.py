@@ -267,6 +267,10 @@ TINY_DEC = dict(vocab=512, embed_dim=128, heads=2, layers=2, ff=512)
 # decoder width differs from the encoder width so the projection is a real Linear (model.py:97-99)
 TINY_DEC96 = dict(vocab=512, embed_dim=192, heads=3, layers=2, ff=384)
 CFG1_DEC = dict(vocab=10000, embed_dim=512, heads=8, layers=6, ff=2048)
+# configs[3]: CLIP ViT-L/14 (224 px -> 257 tokens) + 12L d768 decoder (H = 12, ff = 4d)
+CLIP_L14 = dict(hidden_size=1024, intermediate_size=4096, num_hidden_layers=24, num_attention_heads=16,
+                image_size=224, patch_size=14)
+CFG3_DEC = dict(vocab=10000, embed_dim=768, heads=12, layers=12, ff=3072)
 
 if __name__ == "__main__":
     only = set(sys.argv[1:])
@@ -291,6 +295,9 @@ if __name__ == "__main__":
         # full cfg1 architecture (ViT-B/16 = ViTConfig() defaults + 6L d512 V=10000), batch 2
         run_case("cfg1_b2_patches", "vit", {}, CFG1_DEC, "patches", B=2, cap_len=64, lengths=[64, 41],
                  seed=21, image_size=224, steps=1, full_logits=False)
+    if want("cfg3_b2_patches"):
+        run_case("cfg3_b2_patches", "clip", CLIP_L14, CFG3_DEC, "patches", B=2, cap_len=64, lengths=[64, 37],
+                 seed=41, image_size=224, steps=1, full_logits=False)
     if want("dp2_tiny"):
         run_dp_case("dp2_tiny", "vit", TINY_VIT, TINY_DEC96, B=8, cap_len=20,
                     lengths=[20, 20, 18, 20, 7, 9, 11, 5], seed=31, image_size=224)

@@ -127,7 +127,7 @@ class _GradView:
         return self.s.g(name)
 
 
-@pytest.mark.parametrize("name", ["tiny_vit_patches", "cfg1_b2_patches"])
+@pytest.mark.parametrize("name", ["tiny_vit_patches", "cfg1_b2_patches", "cfg3_b2_patches"])
 def test_train_step_bf16_close_to_reference(name):
     import optim
     meta, T = FX.load(name)
