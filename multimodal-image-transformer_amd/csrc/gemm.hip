@@ -502,6 +502,15 @@ __device__ __forceinline__ void bar_raw() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// compile-time A/B switches of the 256 kernel (tools/build_variants.sh): row-group height of the
+// tile order and the XCD remap
+#ifndef MIT_G256_GROUP
+#define MIT_G256_GROUP 4
+#endif
+#ifndef MIT_G256_NOREMAP
+#define MIT_G256_NOREMAP 0
+#endif
+
 template <int ALAY, int BLAY, int ACT, bool DROP>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                       long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
@@ -513,11 +522,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
 
   const int nbn = (int)((N + B2 - 1) / B2), nbm = (int)((M + B2 - 1) / B2);
   const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
+#if MIT_G256_NOREMAP
+  int bid = blockIdx.x;
+#else
   int bid = xcd_remap(blockIdx.x, nwg);
+#endif
   const int split = bid / ntiles;
   bid -= split * ntiles;
   const long kb = (long)split * kchunk, ke = min(K, kb + kchunk);
-  const int GROUP = 4;
+  const int GROUP = MIT_G256_GROUP;
   const int group_id = bid / (GROUP * nbn);
   const int first_m = group_id * GROUP;
   const int gsize = min(nbm - first_m, GROUP);
