@@ -171,7 +171,7 @@ class ImageTextDataset(torch.utils.data.Dataset):
             print(f"Error loading image {path}: {e}. Returning a dummy item.")
             S = self.pre.size
             return {"image_path": "error_loading_image_path",
-                    "image": torch.from_numpy(self.pre.resize(Image.new("RGB", (S, S)))),
+                    "image": torch.from_numpy(self.pre.resize(Image.new("RGB", (S, S))).copy()),
                     "caption_tokens": torch.full((self.max_seq_len,), config.PAD_TOKEN_ID, dtype=torch.long)}
         ids = pad_or_truncate(self.encode(self.captions[idx]), self.max_seq_len)
         return {"image_path": path, "image": torch.from_numpy(self.pre.resize(image).copy()),
