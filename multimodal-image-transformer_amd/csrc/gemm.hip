@@ -510,6 +510,14 @@ __device__ __forceinline__ void bar_raw() {
 #ifndef MIT_G256_NOREMAP
 #define MIT_G256_NOREMAP 0
 #endif
+// 4 barriers per K-tile (merged phases) with the A half-1 DMA issued one phase earlier is the
+// default (+3-5 % on the 256-tile shapes, profiles/r01_gemm256_schedule_ab.txt); 0 = the 8-phase loop
+#ifndef MIT_G256_PH4
+#define MIT_G256_PH4 1
+#endif
+#ifndef MIT_G256_EARLY_A1
+#define MIT_G256_EARLY_A1 1
+#endif
 
 template <int ALAY, int BLAY, int ACT, bool DROP>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
@@ -613,6 +621,65 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   bar_raw();
   if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
 
+#if MIT_G256_PH4
+  // 4 barriers per K-tile instead of 8: the same reads, DMA issues and waits in the same order,
+  // two quarter-tile MFMA blocks per phase (a 512-cycle MFMA segment per group hides more of the
+  // other group's LDS-read latency)
+  for (int t = 0; t < nk; t += 2) {
+    const bool two = t + 1 < nk;
+    read_a(0, 0);
+    read_b(0, 0, blo);
+    issue(1, 1, t + 1);
+    read_b(0, 1, bhi);
+    issue(0, 0, t + 1);
+#if MIT_G256_EARLY_A1
+    issue(0, 1, t + 1);
+#endif
+    bar_raw();
+    mma(0, 0, blo);
+    mma(0, 1, bhi);
+    bar_raw();
+
+    read_a(0, 1);
+#if !MIT_G256_EARLY_A1
+    issue(0, 1, t + 1);
+#endif
+    wait_dma(issue(1, 0, t + 2));
+    bar_raw();
+    mma(1, 1, bhi);
+    mma(1, 0, blo);
+    bar_raw();
+
+    if (two) {
+      read_a(1, 0);
+      read_b(1, 0, blo);
+    }
+    issue(1, 1, t + 2);
+    if (two) read_b(1, 1, bhi);
+    issue(0, 0, t + 2);
+#if MIT_G256_EARLY_A1
+    issue(0, 1, t + 2);
+#endif
+    bar_raw();
+    if (two) {
+      mma(0, 0, blo);
+      mma(0, 1, bhi);
+    }
+    bar_raw();
+
+    if (two) read_a(1, 1);
+#if !MIT_G256_EARLY_A1
+    issue(0, 1, t + 2);
+#endif
+    wait_dma(issue(1, 0, t + 3));
+    bar_raw();
+    if (two) {
+      mma(1, 1, bhi);
+      mma(1, 0, blo);
+    }
+    bar_raw();
+  }
+#else
   for (int t = 0; t < nk; t += 2) {
     const bool two = t + 1 < nk;  // second K-tile of this iteration exists
     // ---- K-tile t (buffer 0) ----
@@ -667,6 +734,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     if (two) mma(1, 0, blo);
     bar_raw();
   }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wr == 0) bar_raw();  // re-align the groups
   bar_raw();
