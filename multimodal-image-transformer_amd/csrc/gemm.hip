@@ -518,6 +518,9 @@ __device__ __forceinline__ void bar_raw() {
 #ifndef MIT_G256_EARLY_A1
 #define MIT_G256_EARLY_A1 1
 #endif
+#ifndef MIT_G256_PRIO  // raise the wave priority around each MFMA block
+#define MIT_G256_PRIO 1
+#endif
 
 template <int ALAY, int BLAY, int ACT, bool DROP>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
@@ -600,7 +603,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       for (int kk = 0; kk < 2; ++kk) bf[j][kk] = frag<BLAY>(base, (wc & 1) * 64 + jh * 32 + j * 16, kk, lane);
   };
   auto mma = [&](int ih, int jh, bf16x8 (&bf)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
+    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -609,7 +612,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
         for (int j = 0; j < 2; ++j)
           acc[ih * 4 + i][jh * 2 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   // prologue: K-tile 0 (all four halves) and B0 of K-tile 1
