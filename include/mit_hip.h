@@ -124,13 +124,15 @@ int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy, const voi
 int mit_layernorm_param_grads(long rows, long cols, const float* ws, float* dgamma, float* dbeta, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Scaled-dot-product attention, head_dim 64, heads interleaved inside a token row (column h*64).
+ * Scaled-dot-product attention, head_dim Dh in {16, 32, 64, 128} (MFMA kernels at 64, generic
+ * kernels otherwise), heads interleaved inside a token row (column h*Dh). The reference accepts any
+ * nhead dividing d_model (decoder.py:112-118); configs[0] is d128 / 8 heads = head_dim 16.
  * Replaces: encoder MHSA (tf/models/vit/modeling_vit.py:164-189, no mask, scale 1/8);
  * decoder self-attention with the merged causal + key-padding float mask and attention dropout
  * (torch/nn/functional.py:6370-6404, 6553-6566, 6615-6633; masks from utils.py:30-36,66 — the
  * mask is never materialised: key j of batch b is masked iff j > i (causal) or
  * key_tokens[b*tok_batch + j] == pad_idx); decoder cross-attention (no mask).
- * Element strides: X(b, t, h, :) = X + b*X_batch + t*X_row + h*64. lse: f32 [B*H*Lq] (log-sum-exp
+ * Element strides: X(b, t, h, :) = X + b*X_batch + t*X_row + h*Dh. lse: f32 [B*H*Lq] (log-sum-exp
  * of the scaled, masked scores; required by the backward). A fully masked row yields NaN, as in
  * the reference. */
 typedef struct {
@@ -229,17 +231,17 @@ int mit_adamw(long n, float* param, const float* grad, float* m, float* v, void*
  * of the last position, stop at END) by one cached step per token for a whole batch. Every position
  * is read from the DEVICE scalar `pos` (int64), so one step captures into a hipGraph and replays.
  *
- * attention_decode: o[b, h*64:(h+1)*64] = softmax(q_bh . K_bh^T * scale) V_bh for ONE query per
+ * attention_decode: o[b, h*Dh:(h+1)*Dh] = softmax(q_bh . K_bh^T * scale) V_bh for ONE query per
  *   (b, h); keys j < Lk with Lk = *pos + 1 when pos != NULL (causal self-attention over the cache),
  *   else the fixed Lk (cross-attention over the image memory). Key j is masked when
  *   key_tokens[b*tok_batch + j] == pad_idx (the reference's key-padding mask, utils.py:47-70), when
- *   key_tokens != NULL. Head dim 64, heads at column h*64 of each row. All keys masked -> NaN.
+ *   key_tokens != NULL. Head dim Dh in {16, 32, 64, 128}, heads at column h*Dh. All keys masked -> NaN.
  * kv_store: cache[b*c_batch + (*pos)*c_row + e] = src[b*s_batch + e], e < n.
  * embed_decode: out[b, :] = table[ids[b*ld_ids + *pos]] * scale + pe[*pos]   (decoder.py:168-171)
  * greedy_pick: ids[b*ld_ids + *pos + 1] = argmax_v logits[b*ld + v] (first maximal index, like
  *   torch.argmax, model.py:236) for rows not yet finished (finished rows get pad_id); a row whose
  *   pick is end_id sets finished[b] = 1 and increments *n_finished (int32 device scalars). */
-int mit_attention_decode(int dtype, long B, long H, const void* q, long q_batch, const void* k, long k_row,
+int mit_attention_decode(int dtype, long B, long H, long Dh, const void* q, long q_batch, const void* k, long k_row,
                          long k_batch, const void* v, long v_row, long v_batch, void* o, long o_batch, long Lk,
                          const int64_t* pos, const int64_t* key_tokens, long tok_batch, int pad_idx, float scale,
                          void* stream);

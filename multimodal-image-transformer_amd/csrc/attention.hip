@@ -1,4 +1,4 @@
-// Scaled-dot-product attention, head_dim 64.
+// Scaled-dot-product attention: MFMA kernels for head_dim 64, generic kernels for 16/32/64/128.
 //
 // Semantics (the reference's SDPA call, torch/nn/functional.py:6615-6633):
 //   s_ij = scale * q_i . k_j  (+ -inf where j > i if causal, or key j is PAD)
@@ -49,23 +49,27 @@ __device__ __forceinline__ bool key_masked(const AttnK& a, long b, long i, long 
 }
 
 // ------------------------------------------------------------------------------------------------
-// simple forward
+// simple forward: one query row per thread, fp32 math, K/V tiles of 64 keys broadcast from LDS.
+// Any dtype and any head_dim DH in {16, 32, 64, 128} (the decoder of configs[0] is d128 / 8 heads).
+// Scores are evaluated in chunks of KC keys (KC = 16 at DH = 128 keeps q, o and the chunk's scores
+// in registers).
 // ------------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int DH>
 __global__ __launch_bounds__(64) void attn_fwd_simple(long H, long Lq, long Lk, AttnK a) {
-  __shared__ float Ks[64][D + 1];
-  __shared__ float Vs[64][D + 1];
+  constexpr int KC = DH <= 64 ? 64 : 16;
+  __shared__ float Ks[64][DH + 1];
+  __shared__ float Vs[64][DH + 1];
   const int tid = threadIdx.x;
   const long b = blockIdx.z, h = blockIdx.y, i = (long)blockIdx.x * 64 + tid;
   const bool live = i < Lq;
-  const T* Q = (const T*)a.q + b * a.q_batch + h * D;
-  const T* K = (const T*)a.k + b * a.k_batch + h * D;
-  const T* V = (const T*)a.v + b * a.v_batch + h * D;
+  const T* Q = (const T*)a.q + b * a.q_batch + h * DH;
+  const T* K = (const T*)a.k + b * a.k_batch + h * DH;
+  const T* V = (const T*)a.v + b * a.v_batch + h * DH;
   const uint64_t key = a.dropout ? site_key(a.seed, a.site) : 0ull;
   const uint64_t rowbase = ((uint64_t)(b * H + h) * (uint64_t)Lq + (uint64_t)i) * (uint64_t)Lk;
-  float q[D], o[D];
+  float q[DH], o[DH];
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
+  for (int d = 0; d < DH; ++d) {
     q[d] = live ? to_f(Q[i * a.q_row + d]) * a.scale : 0.f;
     o[d] = 0.f;
   }
@@ -73,8 +77,8 @@ __global__ __launch_bounds__(64) void attn_fwd_simple(long H, long Lq, long Lk, 
   for (long j0 = 0; j0 < Lk; j0 += 64) {
     const int nj = (int)min((long)64, Lk - j0);
     __syncthreads();
-    for (int idx = tid; idx < 64 * D; idx += 64) {
-      const int r = idx / D, c = idx % D;
+    for (int idx = tid; idx < 64 * DH; idx += 64) {
+      const int r = idx / DH, c = idx % DH;
       float kv = 0.f, vv = 0.f;
       if (r < nj) {
         kv = to_f(K[(j0 + r) * a.k_row + c]);
@@ -85,45 +89,47 @@ __global__ __launch_bounds__(64) void attn_fwd_simple(long H, long Lq, long Lk, 
     }
     __syncthreads();
     if (!live) continue;
-    float s[64];
-    float tmax = -INFINITY;
+    for (int c0 = 0; c0 < 64; c0 += KC) {
+      float s[KC];
+      float tmax = -INFINITY;
 #pragma unroll
-    for (int jj = 0; jj < 64; ++jj) {
-      float acc = 0.f;
+      for (int jj = 0; jj < KC; ++jj) {
+        float acc = 0.f;
 #pragma unroll
-      for (int d = 0; d < D; ++d) acc = fmaf(q[d], Ks[jj][d], acc);
-      const bool msk = (jj >= nj) || key_masked(a, b, i, j0 + jj);
-      s[jj] = msk ? -INFINITY : acc;
-      tmax = fmaxf(tmax, s[jj]);
-    }
-    const float mnew = fmaxf(m, tmax);
-    const float corr = (mnew == -INFINITY) ? 1.f : __expf(m - mnew);
-    l *= corr;
-#pragma unroll
-    for (int d = 0; d < D; ++d) o[d] *= corr;
-#pragma unroll
-    for (int jj = 0; jj < 64; ++jj) {
-      const float p = (s[jj] == -INFINITY) ? 0.f : __expf(s[jj] - mnew);
-      l += p;
-      float pd = p;
-      if (a.dropout) pd *= drop_mul(key, rowbase + (uint64_t)(j0 + jj), a.thresh, a.dscale);
-      if (pd != 0.f) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) o[d] = fmaf(pd, Vs[jj][d], o[d]);
+        for (int d = 0; d < DH; ++d) acc = fmaf(q[d], Ks[c0 + jj][d], acc);
+        const bool msk = (c0 + jj >= nj) || key_masked(a, b, i, j0 + c0 + jj);
+        s[jj] = msk ? -INFINITY : acc;
+        tmax = fmaxf(tmax, s[jj]);
       }
+      const float mnew = fmaxf(m, tmax);
+      const float corr = (mnew == -INFINITY) ? 1.f : __expf(m - mnew);
+      l *= corr;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) o[d] *= corr;
+#pragma unroll
+      for (int jj = 0; jj < KC; ++jj) {
+        const float p = (s[jj] == -INFINITY) ? 0.f : __expf(s[jj] - mnew);
+        l += p;
+        float pd = p;
+        if (a.dropout) pd *= drop_mul(key, rowbase + (uint64_t)(j0 + c0 + jj), a.thresh, a.dscale);
+        if (pd != 0.f) {
+#pragma unroll
+          for (int d = 0; d < DH; ++d) o[d] = fmaf(pd, Vs[c0 + jj][d], o[d]);
+        }
+      }
+      m = mnew;
     }
-    m = mnew;
   }
   if (!live) return;
   const float inv = 1.0f / l;  // l == 0 (fully masked row) -> inf * 0 = NaN, as the reference
-  T* O = (T*)a.o + b * a.o_batch + i * a.o_row + h * D;
+  T* O = (T*)a.o + b * a.o_batch + i * a.o_row + h * DH;
 #pragma unroll
-  for (int d = 0; d < D; ++d) O[d] = from_f<T>(o[d] * inv);
+  for (int d = 0; d < DH; ++d) O[d] = from_f<T>(o[d] * inv);
   if (a.lse) a.lse[(b * H + h) * Lq + i] = m + __logf(l);
 }
 
 // ------------------------------------------------------------------------------------------------
-// simple backward: (1) dQ + delta, thread per query; (2) dK/dV, thread per key
+// simple backward: (1) dQ + delta, thread per query; (2) dK/dV, thread per key. Any head_dim DH.
 // ------------------------------------------------------------------------------------------------
 struct AttnG {
   const void* dout;
@@ -137,25 +143,25 @@ struct AttnG {
   float* delta;
 };
 
-template <typename T>
+template <typename T, int DH>
 __global__ __launch_bounds__(64) void attn_bwd_dq_simple(long H, long Lq, long Lk, AttnK a, AttnG g) {
-  __shared__ float Ks[64][D + 1];
-  __shared__ float Vs[64][D + 1];
+  __shared__ float Ks[64][DH + 1];
+  __shared__ float Vs[64][DH + 1];
   const int tid = threadIdx.x;
   const long b = blockIdx.z, h = blockIdx.y, i = (long)blockIdx.x * 64 + tid;
   const bool live = i < Lq;
-  const T* Q = (const T*)a.q + b * a.q_batch + h * D;
-  const T* K = (const T*)a.k + b * a.k_batch + h * D;
-  const T* V = (const T*)a.v + b * a.v_batch + h * D;
-  const T* O = (const T*)a.o + b * a.o_batch + h * D;
-  const T* dO = (const T*)g.dout + b * g.do_batch + h * D;
+  const T* Q = (const T*)a.q + b * a.q_batch + h * DH;
+  const T* K = (const T*)a.k + b * a.k_batch + h * DH;
+  const T* V = (const T*)a.v + b * a.v_batch + h * DH;
+  const T* O = (const T*)a.o + b * a.o_batch + h * DH;
+  const T* dO = (const T*)g.dout + b * g.do_batch + h * DH;
   const uint64_t key = a.dropout ? site_key(a.seed, a.site) : 0ull;
   const uint64_t rowbase = ((uint64_t)(b * H + h) * (uint64_t)Lq + (uint64_t)i) * (uint64_t)Lk;
-  float q[D], dout[D], dq[D];
+  float q[DH], dout[DH], dq[DH];
   float delta = 0.f, lse = 0.f;
   if (live) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
+    for (int d = 0; d < DH; ++d) {
       q[d] = to_f(Q[i * a.q_row + d]);
       dout[d] = to_f(dO[i * g.do_row + d]);
       delta = fmaf(dout[d], to_f(O[i * a.o_row + d]), delta);
@@ -167,8 +173,8 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_simple(long H, long Lq, long L
   for (long j0 = 0; j0 < Lk; j0 += 64) {
     const int nj = (int)min((long)64, Lk - j0);
     __syncthreads();
-    for (int idx = tid; idx < 64 * D; idx += 64) {
-      const int r = idx / D, c = idx % D;
+    for (int idx = tid; idx < 64 * DH; idx += 64) {
+      const int r = idx / DH, c = idx % DH;
       float kv = 0.f, vv = 0.f;
       if (r < nj) {
         kv = to_f(K[(j0 + r) * a.k_row + c]);
@@ -183,7 +189,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_simple(long H, long Lq, long L
       if (key_masked(a, b, i, j0 + jj)) continue;
       float s = 0.f, dp = 0.f;
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
+      for (int d = 0; d < DH; ++d) {
         s = fmaf(q[d], Ks[jj][d], s);
         dp = fmaf(dout[d], Vs[jj][d], dp);
       }
@@ -191,45 +197,45 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_simple(long H, long Lq, long L
       if (a.dropout) dp *= drop_mul(key, rowbase + (uint64_t)(j0 + jj), a.thresh, a.dscale);
       const float ds = p * (dp - delta);
 #pragma unroll
-      for (int d = 0; d < D; ++d) dq[d] = fmaf(ds, Ks[jj][d], dq[d]);
+      for (int d = 0; d < DH; ++d) dq[d] = fmaf(ds, Ks[jj][d], dq[d]);
     }
   }
   if (!live) return;
-  T* DQ = (T*)g.dq + b * g.dq_batch + i * g.dq_row + h * D;
+  T* DQ = (T*)g.dq + b * g.dq_batch + i * g.dq_row + h * DH;
 #pragma unroll
-  for (int d = 0; d < D; ++d) DQ[d] = from_f<T>(dq[d] * a.scale);
+  for (int d = 0; d < DH; ++d) DQ[d] = from_f<T>(dq[d] * a.scale);
 }
 
-template <typename T>
+template <typename T, int DH>
 __global__ __launch_bounds__(64) void attn_bwd_dkv_simple(long H, long Lq, long Lk, AttnK a, AttnG g) {
-  __shared__ float Kp[64][D + 1];  // this block's keys, one private row per thread
-  __shared__ float Vp[64][D + 1];
-  __shared__ float Qs[64][D + 1];  // query tile (broadcast reads)
-  __shared__ float Ds[64][D + 1];  // dO tile
+  __shared__ float Kp[64][DH + 1];  // this block's keys, one private row per thread
+  __shared__ float Vp[64][DH + 1];
+  __shared__ float Qs[64][DH + 1];  // query tile (broadcast reads)
+  __shared__ float Ds[64][DH + 1];  // dO tile
   __shared__ float Ls[64], Dl[64];
   const int tid = threadIdx.x;
   const long b = blockIdx.z, h = blockIdx.y, j = (long)blockIdx.x * 64 + tid;
   const bool live = j < Lk;
-  const T* Q = (const T*)a.q + b * a.q_batch + h * D;
-  const T* K = (const T*)a.k + b * a.k_batch + h * D;
-  const T* V = (const T*)a.v + b * a.v_batch + h * D;
-  const T* dO = (const T*)g.dout + b * g.do_batch + h * D;
+  const T* Q = (const T*)a.q + b * a.q_batch + h * DH;
+  const T* K = (const T*)a.k + b * a.k_batch + h * DH;
+  const T* V = (const T*)a.v + b * a.v_batch + h * DH;
+  const T* dO = (const T*)g.dout + b * g.do_batch + h * DH;
   const uint64_t key = a.dropout ? site_key(a.seed, a.site) : 0ull;
-  for (int idx = tid; idx < 64 * D; idx += 64) {
-    const int r = idx / D, c = idx % D;
+  for (int idx = tid; idx < 64 * DH; idx += 64) {
+    const int r = idx / DH, c = idx % DH;
     const long jj = (long)blockIdx.x * 64 + r;
     Kp[r][c] = jj < Lk ? to_f(K[jj * a.k_row + c]) : 0.f;
     Vp[r][c] = jj < Lk ? to_f(V[jj * a.v_row + c]) : 0.f;
   }
   const bool kpad = live && a.tok && a.tok[b * a.tok_batch + j] == a.pad;
-  float dk[D], dv[D];
+  float dk[DH], dv[DH];
 #pragma unroll
-  for (int d = 0; d < D; ++d) dk[d] = dv[d] = 0.f;
+  for (int d = 0; d < DH; ++d) dk[d] = dv[d] = 0.f;
   for (long i0 = 0; i0 < Lq; i0 += 64) {
     const int ni = (int)min((long)64, Lq - i0);
     __syncthreads();
-    for (int idx = tid; idx < 64 * D; idx += 64) {
-      const int r = idx / D, c = idx % D;
+    for (int idx = tid; idx < 64 * DH; idx += 64) {
+      const int r = idx / DH, c = idx % DH;
       Qs[r][c] = r < ni ? to_f(Q[(i0 + r) * a.q_row + c]) : 0.f;
       Ds[r][c] = r < ni ? to_f(dO[(i0 + r) * g.do_row + c]) : 0.f;
     }
@@ -244,7 +250,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_simple(long H, long Lq, long 
       if (a.causal && j > i) continue;
       float s = 0.f, dp = 0.f;
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
+      for (int d = 0; d < DH; ++d) {
         s = fmaf(Qs[ii][d], Kp[tid][d], s);
         dp = fmaf(Ds[ii][d], Vp[tid][d], dp);
       }
@@ -255,17 +261,17 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_simple(long H, long Lq, long 
       const float pd = p * mul;
       const float ds = p * (dp * mul - Dl[ii]);
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
+      for (int d = 0; d < DH; ++d) {
         dv[d] = fmaf(pd, Ds[ii][d], dv[d]);
         dk[d] = fmaf(ds, Qs[ii][d], dk[d]);
       }
     }
   }
   if (!live) return;
-  T* DK = (T*)g.dk + b * g.dk_batch + j * g.dk_row + h * D;
-  T* DV = (T*)g.dv + b * g.dv_batch + j * g.dv_row + h * D;
+  T* DK = (T*)g.dk + b * g.dk_batch + j * g.dk_row + h * DH;
+  T* DV = (T*)g.dv + b * g.dv_batch + j * g.dv_row + h * DH;
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
+  for (int d = 0; d < DH; ++d) {
     DK[d] = from_f<T>(dk[d] * a.scale);
     DV[d] = from_f<T>(dv[d]);
   }
@@ -1014,6 +1020,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   }
 }
 
+// head_dim dispatch for the generic kernels: DH in {16, 32, 64, 128}
+#define DISPATCH_DH(dh, ...)                    \
+  do {                                          \
+    switch (dh) {                               \
+      case 16: { constexpr int DH = 16; __VA_ARGS__; } break;   \
+      case 32: { constexpr int DH = 32; __VA_ARGS__; } break;   \
+      case 64: { constexpr int DH = 64; __VA_ARGS__; } break;   \
+      default: { constexpr int DH = 128; __VA_ARGS__; } break;  \
+    }                                           \
+  } while (0)
+
+inline bool head_dim_ok(long dh) { return dh == 16 || dh == 32 || dh == 64 || dh == 128; }
+
 AttnK make_k(const mit_attn_args* x) {
   AttnK a;
   a.q = x->q; a.q_row = x->q_row; a.q_batch = x->q_batch;
@@ -1034,13 +1053,15 @@ AttnK make_k(const mit_attn_args* x) {
 extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, long Dh, const mit_attn_args* x,
                                  void* stream) {
   MIT_CHECK_ARG(x && x->q && x->k && x->v && x->o, "mit_attention_fwd: null pointer");
-  MIT_CHECK_ARG(Dh == D, "mit_attention_fwd: head_dim %ld unsupported (64 only)", Dh);
+  MIT_CHECK_ARG(head_dim_ok(Dh), "mit_attention_fwd: head_dim %ld unsupported (16, 32, 64, 128)", Dh);
   if (B <= 0 || H <= 0 || Lq <= 0) return MIT_OK;
   MIT_CHECK_ARG(Lk > 0, "mit_attention_fwd: Lk must be > 0");
   AttnK a = make_k(x);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((Lq + 63) / 64), (unsigned)H, (unsigned)B);
-  const bool mfma_ok = dtype == MIT_BF16 && x->q_row % 8 == 0 && x->q_batch % 8 == 0 && x->k_row % 8 == 0 &&
+  // the MFMA kernels are written for head_dim 64 (every ViT / CLIP tower and the 512/768-wide
+  // decoders); other head dims run the generic kernels
+  const bool mfma_ok = Dh == D && dtype == MIT_BF16 && x->q_row % 8 == 0 && x->q_batch % 8 == 0 && x->k_row % 8 == 0 &&
                        x->k_batch % 8 == 0 && x->v_row % 8 == 0 && x->v_batch % 8 == 0 && x->o_row % 4 == 0 &&
                        x->o_batch % 4 == 0 && ((uintptr_t)x->q | (uintptr_t)x->k | (uintptr_t)x->v) % 16 == 0 &&
                        ((uintptr_t)x->o % 8) == 0 && getenv("MIT_ATTN_SIMPLE") == nullptr;
@@ -1074,10 +1095,11 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
     } else {
       hipLaunchKernelGGL(attn_fwd_mfma, grid, dim3(256), 0, s, H, Lq, Lk, a, (int)kb, (int)vb);
     }
-  } else if (dtype == MIT_BF16)
-    hipLaunchKernelGGL(attn_fwd_simple<bf16>, grid, dim3(64), 0, s, H, Lq, Lk, a);
-  else
-    hipLaunchKernelGGL(attn_fwd_simple<float>, grid, dim3(64), 0, s, H, Lq, Lk, a);
+  } else if (dtype == MIT_BF16) {
+    DISPATCH_DH(Dh, hipLaunchKernelGGL((attn_fwd_simple<bf16, DH>), grid, dim3(64), 0, s, H, Lq, Lk, a));
+  } else {
+    DISPATCH_DH(Dh, hipLaunchKernelGGL((attn_fwd_simple<float, DH>), grid, dim3(64), 0, s, H, Lq, Lk, a));
+  }
   MIT_LAUNCH_CHECK("mit_attention_fwd");
   return MIT_OK;
 }
@@ -1086,7 +1108,7 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
                                  const mit_attn_grads* gg, void* stream) {
   MIT_CHECK_ARG(x && gg && x->q && x->k && x->v && x->o && x->lse, "mit_attention_bwd: null forward pointer");
   MIT_CHECK_ARG(gg->dout && gg->dq && gg->dk && gg->dv && gg->delta_ws, "mit_attention_bwd: null grad pointer");
-  MIT_CHECK_ARG(Dh == D, "mit_attention_bwd: head_dim %ld unsupported (64 only)", Dh);
+  MIT_CHECK_ARG(head_dim_ok(Dh), "mit_attention_bwd: head_dim %ld unsupported (16, 32, 64, 128)", Dh);
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return MIT_OK;
   AttnK a = make_k(x);
   AttnG g;
@@ -1099,7 +1121,7 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
   dim3 gq((unsigned)((Lq + 63) / 64), (unsigned)H, (unsigned)B);
   dim3 gk((unsigned)((Lk + 63) / 64), (unsigned)H, (unsigned)B);
   auto al = [](const void* p, int n) { return ((uintptr_t)p % n) == 0; };
-  const bool mfma_ok = dtype == MIT_BF16 && x->q_row % 8 == 0 && x->q_batch % 8 == 0 && x->k_row % 8 == 0 &&
+  const bool mfma_ok = Dh == D && dtype == MIT_BF16 && x->q_row % 8 == 0 && x->q_batch % 8 == 0 && x->k_row % 8 == 0 &&
                        x->k_batch % 8 == 0 && x->v_row % 8 == 0 && x->v_batch % 8 == 0 && x->o_row % 8 == 0 &&
                        x->o_batch % 8 == 0 && gg->do_row % 8 == 0 && gg->do_batch % 8 == 0 && gg->dq_row % 4 == 0 &&
                        gg->dq_batch % 4 == 0 && gg->dk_row % 4 == 0 && gg->dk_batch % 4 == 0 && gg->dv_row % 4 == 0 &&
@@ -1132,11 +1154,11 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
       hipLaunchKernelGGL(attn_bwd_dkv_mfma, gk, dim3(256), 0, s, H, Lq, Lk, a, g, nb);
     }
   } else if (dtype == MIT_BF16) {
-    hipLaunchKernelGGL(attn_bwd_dq_simple<bf16>, gq, dim3(64), 0, s, H, Lq, Lk, a, g);
-    hipLaunchKernelGGL(attn_bwd_dkv_simple<bf16>, gk, dim3(64), 0, s, H, Lq, Lk, a, g);
+    DISPATCH_DH(Dh, hipLaunchKernelGGL((attn_bwd_dq_simple<bf16, DH>), gq, dim3(64), 0, s, H, Lq, Lk, a, g);
+                    hipLaunchKernelGGL((attn_bwd_dkv_simple<bf16, DH>), gk, dim3(64), 0, s, H, Lq, Lk, a, g));
   } else {
-    hipLaunchKernelGGL(attn_bwd_dq_simple<float>, gq, dim3(64), 0, s, H, Lq, Lk, a, g);
-    hipLaunchKernelGGL(attn_bwd_dkv_simple<float>, gk, dim3(64), 0, s, H, Lq, Lk, a, g);
+    DISPATCH_DH(Dh, hipLaunchKernelGGL((attn_bwd_dq_simple<float, DH>), gq, dim3(64), 0, s, H, Lq, Lk, a, g);
+                    hipLaunchKernelGGL((attn_bwd_dkv_simple<float, DH>), gk, dim3(64), 0, s, H, Lq, Lk, a, g));
   }
   MIT_LAUNCH_CHECK("mit_attention_bwd");
   return MIT_OK;

@@ -59,7 +59,9 @@ __device__ __forceinline__ void merge(float& m, float& l, float* acc, float m2, 
   m = mn;
 }
 
-template <typename T>
+// head_dim DH in {16, 32, 64, 128}: LPR = DH / 8 lanes per key row (8 elements each), KPW = 64 / LPR
+// keys per wave iteration
+template <typename T, int DH>
 __global__ __launch_bounds__(256) void attn_decode_kernel(long H, const T* __restrict__ q, long q_batch,
                                                           const T* __restrict__ k, long k_row, long k_batch,
                                                           const T* __restrict__ v, long v_row, long v_batch,
@@ -67,23 +69,24 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(long H, const T* __res
                                                           const int64_t* __restrict__ pos,
                                                           const int64_t* __restrict__ key_tokens, long tok_batch,
                                                           int pad_idx, float scale) {
-  __shared__ float red[4][2 + 64];
+  constexpr int LPR = DH / 8, KPW = 64 / LPR;
+  __shared__ float red[4][2 + DH];
   const int bh = blockIdx.x;
   const long b = bh / H, h = bh % H;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 3, c = lane & 7;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane / LPR, c = lane % LPR;
   const long Lk = pos ? (*pos + 1) : lk_fixed;
 
   float qv[8];
-  load8<T>(q + b * q_batch + h * 64 + c * 8, qv);
+  load8<T>(q + b * q_batch + h * DH + c * 8, qv);
 #pragma unroll
   for (int i = 0; i < 8; ++i) qv[i] *= scale * kLog2e;
 
-  const T* kb = k + b * k_batch + h * 64 + c * 8;
-  const T* vb = v + b * v_batch + h * 64 + c * 8;
+  const T* kb = k + b * k_batch + h * DH + c * 8;
+  const T* vb = v + b * v_batch + h * DH + c * 8;
   const int64_t* tb = key_tokens ? key_tokens + b * tok_batch : nullptr;
   float m = kNegBig, l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  // key j = (it * 4 + w) * 8 + g: the four waves sweep interleaved 8-key slabs
-  for (long j = (long)w * 8 + g; j - g < Lk; j += 32) {
+  // key j = (it * 4 + w) * KPW + g: the four waves sweep interleaved KPW-key slabs
+  for (long j = (long)w * KPW + g; j - g < Lk; j += 4 * KPW) {
     const bool ok = j < Lk && (!tb || tb[j] != pad_idx);
     float kf[8], vf[8];
     if (j < Lk) {
@@ -96,9 +99,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(long H, const T* __res
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) s = fmaf(qv[i], kf[i], s);
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
+#pragma unroll
+    for (int x = 1; x < LPR; x <<= 1) s += __shfl_xor(s, x, 64);
     if (!ok) s = -INFINITY;
     const float mn = fmaxf(m, s);
     const float corr = exp2f(m - mn), p = exp2f(s - mn);
@@ -107,9 +109,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(long H, const T* __res
     for (int i = 0; i < 8; ++i) acc[i] = fmaf(p, vf[i], acc[i] * corr);
     m = mn;
   }
-  // merge the 8 key groups of the wave (lanes with equal c)
+  // merge the KPW key groups of the wave (lanes with equal c)
 #pragma unroll
-  for (int x = 8; x < 64; x <<= 1) {
+  for (int x = LPR; x < 64; x <<= 1) {
     float a2[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) a2[i] = __shfl_xor(acc[i], x, 64);
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(long H, const T* __res
     const float inv = 1.0f / l;  // all keys masked -> 0/0 = NaN, as the reference's softmax
 #pragma unroll
     for (int i = 0; i < 8; ++i) out[i] = acc[i] * inv;
-    store8<T>(o + b * o_batch + h * 64 + c * 8, out);
+    store8<T>(o + b * o_batch + h * DH + c * 8, out);
   }
 }
 
@@ -238,11 +240,12 @@ inline unsigned grid_for(long n, int block = 256, long cap = 8192) {
     }                                 \
   } while (0)
 
-extern "C" int mit_attention_decode(int dtype, long B, long H, const void* q, long q_batch, const void* k, long k_row,
-                                    long k_batch, const void* v, long v_row, long v_batch, void* o, long o_batch,
-                                    long Lk, const int64_t* pos, const int64_t* key_tokens, long tok_batch,
-                                    int pad_idx, float scale, void* stream) {
+extern "C" int mit_attention_decode(int dtype, long B, long H, long Dh, const void* q, long q_batch, const void* k,
+                                    long k_row, long k_batch, const void* v, long v_row, long v_batch, void* o,
+                                    long o_batch, long Lk, const int64_t* pos, const int64_t* key_tokens,
+                                    long tok_batch, int pad_idx, float scale, void* stream) {
   MIT_CHECK_ARG(q && k && v && o, "mit_attention_decode: null pointer");
+  MIT_CHECK_ARG(Dh == 16 || Dh == 32 || Dh == 64 || Dh == 128, "mit_attention_decode: head_dim %ld unsupported", Dh);
   MIT_CHECK_ARG(dtype == MIT_BF16 || dtype == MIT_F32, "mit_attention_decode: bad dtype");
   MIT_CHECK_ARG(pos || Lk > 0, "mit_attention_decode: need a device position or Lk > 0");
   const long esz = dtype == MIT_BF16 ? 2 : 4;
@@ -251,10 +254,18 @@ extern "C" int mit_attention_decode(int dtype, long B, long H, const void* q, lo
                     (v_row * esz) % 16 == 0 && (v_batch * esz) % 16 == 0 && (o_batch * esz) % 16 == 0,
                 "mit_attention_decode: rows must be 16-B aligned");
   if (B <= 0 || H <= 0) return MIT_OK;
-  DISPATCH_DT(dtype, hipLaunchKernelGGL(attn_decode_kernel<T>, dim3((unsigned)(B * H)), dim3(256), 0,
-                                        (hipStream_t)stream, H, (const T*)q, q_batch, (const T*)k, k_row, k_batch,
-                                        (const T*)v, v_row, v_batch, (T*)o, o_batch, Lk, pos, key_tokens, tok_batch,
-                                        pad_idx, scale));
+#define MIT_DECODE_LAUNCH(DH_)                                                                                       \
+  DISPATCH_DT(dtype, hipLaunchKernelGGL((attn_decode_kernel<T, DH_>), dim3((unsigned)(B * H)), dim3(256), 0,          \
+                                        (hipStream_t)stream, H, (const T*)q, q_batch, (const T*)k, k_row, k_batch,    \
+                                        (const T*)v, v_row, v_batch, (T*)o, o_batch, Lk, pos, key_tokens, tok_batch, \
+                                        pad_idx, scale))
+  switch (Dh) {
+    case 16: MIT_DECODE_LAUNCH(16); break;
+    case 32: MIT_DECODE_LAUNCH(32); break;
+    case 64: MIT_DECODE_LAUNCH(64); break;
+    default: MIT_DECODE_LAUNCH(128); break;
+  }
+#undef MIT_DECODE_LAUNCH
   MIT_LAUNCH_CHECK("mit_attention_decode");
   return MIT_OK;
 }

@@ -164,7 +164,9 @@ __global__ __launch_bounds__(256) void ce_kernel(long V, T* logits, long ld, con
 // bf16 rows with V <= CE_NCH * 512 (the decoder head, V = 10000): one wave per row, the row held in
 // registers (CE_NCH x 16-B loads per lane), so HBM sees one read and one write of the logits; each
 // row's loss goes to row_loss[row] and ce_sum adds them up in row order (deterministic, no
-// single-address float atomics: 4032 of those serialised cost ~100 us).
+// single-address float atomics: 4032 of those serialised cost ~100 us). V need not be a multiple
+// of 8 when ld is (the head padded to Vp = round8(V) columns): the tail of the last 16-B chunk is
+// masked out of the softmax and its gradient is written as 0.
 constexpr int CE_NCH = 20;
 __global__ __launch_bounds__(256) void ce_rows_bf16(long rows, long V, bf16* logits, long ld,
                                                      const int64_t* __restrict__ targets, int ignore,
@@ -185,19 +187,25 @@ __global__ __launch_bounds__(256) void ce_rows_bf16(long rows, long V, bf16* log
   const float xt = (!ign && tg >= 0 && tg < V) ? (float)x[tg] : 0.f;
   float mx = -INFINITY;
 #pragma unroll
-  for (int c = 0; c < CE_NCH; ++c)
-    if ((long)c * 512 + lane * 8 < V) {
+  for (int c = 0; c < CE_NCH; ++c) {
+    const long j = (long)c * 512 + lane * 8;
+    if (j < V) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) mx = fmaxf(mx, (float)v[c][k]);
+      for (int k = 0; k < 8; ++k)
+        if (j + k < V) mx = fmaxf(mx, (float)v[c][k]);
     }
+  }
   mx = wave_max(mx);
   float se = 0.f;
 #pragma unroll
-  for (int c = 0; c < CE_NCH; ++c)
-    if ((long)c * 512 + lane * 8 < V) {
+  for (int c = 0; c < CE_NCH; ++c) {
+    const long j = (long)c * 512 + lane * 8;
+    if (j < V) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) se += __expf((float)v[c][k] - mx);
+      for (int k = 0; k < 8; ++k)
+        if (j + k < V) se += __expf((float)v[c][k] - mx);
     }
+  }
   se = wave_sum(se);
   const float lse = mx + __logf(se);
   if (lane == 0) row_loss[row] = ign ? 0.f : lse - xt;
@@ -213,7 +221,7 @@ __global__ __launch_bounds__(256) void ce_rows_bf16(long rows, long V, bf16* log
       for (int k = 0; k < 8; ++k) {
         float p = __expf((float)v[c][k] - mx) * inv;
         if (j + k == tg) p -= 1.0f;
-        o[k] = (bf16)(p * gs);
+        o[k] = (j + k < V) ? (bf16)(p * gs) : (bf16)0.f;
       }
       *(bf16x8*)(x + j) = o;
     }
@@ -446,7 +454,7 @@ extern "C" int mit_cross_entropy(int dtype, long rows, long V, void* logits, lon
   MIT_CHECK_ARG(logits && targets && loss_sum && (!want_grad || count), "mit_cross_entropy: null pointer");
   MIT_CHECK_ARG(ld >= V, "mit_cross_entropy: ld < V");
   if (rows <= 0) return MIT_OK;
-  if (row_loss && dtype == MIT_BF16 && V <= CE_NCH * 512 && V % 8 == 0 && ld % 8 == 0 &&
+  if (row_loss && dtype == MIT_BF16 && V <= CE_NCH * 512 && ld % 8 == 0 && (V % 8 == 0 || ld >= (V + 7) / 8 * 8) &&
       ((uintptr_t)logits % 16) == 0) {
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(ce_rows_bf16, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, rows, V, (bf16*)logits, ld,

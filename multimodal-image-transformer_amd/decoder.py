@@ -43,9 +43,19 @@ def sinusoidal_pe(max_len: int, d: int) -> torch.Tensor:
     return pe
 
 
+def padded_vocab(V: int) -> int:
+    """The vocabulary head is stored with Vp = round8(V) rows: the bf16 GEMMs need the contiguous
+    extent of every operand (the fc_out weight gradient has M = V, lda = V) to be a multiple of 8,
+    and the reference sizes V from the trained tokenizer (tokenizer.py:200-201, any size). The pad
+    rows of fc_out are zero and stay zero (their gradient is exactly 0, so AdamW never moves them);
+    the pad logit columns are 0 and never reach the caller, the loss or argmax."""
+    return (V + 7) // 8 * 8
+
+
 def decoder_entries(V: int, d: int, L: int, F: int, proj_in: Optional[int]) -> List[Tuple[str, Tuple[int, ...]]]:
     """Flat-buffer layout in backward-completion order (see params.py)."""
-    e = [("fc_out.weight", (V, d)), ("fc_out.bias", (V,))]
+    Vp = padded_vocab(V)
+    e = [("fc_out.weight", (Vp, d)), ("fc_out.bias", (Vp,))]
     for i in reversed(range(L)):
         p = f"layers.{i}."
         e += [(p + "linear2.weight", (d, F)), (p + "linear2.bias", (d,)), (p + "linear1.weight", (F, d)),
@@ -120,8 +130,9 @@ def flat_to_reference(store: FlatParams, L: int, d: int, prefix: str = "decoder.
         for s in ("linear1", "linear2", "norm1", "norm2", "norm3"):
             sd[r + s + ".weight"] = p(q + s + ".weight")
             sd[r + s + ".bias"] = p(q + s + ".bias")
-    sd[prefix + "fc_out.weight"] = p("fc_out.weight")
-    sd[prefix + "fc_out.bias"] = p("fc_out.bias")
+    V = getattr(store, "vocab", None)
+    sd[prefix + "fc_out.weight"] = p("fc_out.weight")[:V]
+    sd[prefix + "fc_out.bias"] = p("fc_out.bias")[:V]
     return sd
 
 
@@ -136,7 +147,7 @@ class _Acts:
         self.x0 = e(R, d)
         self.y = e(R, d)
         self.kv = e(B * S, L * 2 * d)
-        self.logits = e(R, V)
+        self.logits = e(R, padded_vocab(V))  # padded head columns: row stride Vp
         nl = L if train else 1  # eval keeps one set of per-layer buffers and reuses it
         self.qkv = [e(R, 3 * d) for _ in range(nl)]
         self.os = [e(R, d) for _ in range(nl)]
@@ -157,9 +168,10 @@ class _Acts:
         # combine their K slices in-launch; weight-gradient / long-K GEMMs reduce in a second launch.
         # Zero-filled once: its first 4 KiB are tile counters the kernels leave at zero.
         E = proj_in or d
-        shapes = [(R, d, d), (R, d, F), (R, d, 3 * d), (R, d, V)]
+        Vp = padded_vocab(V)
+        shapes = [(R, d, d), (R, d, F), (R, d, 3 * d), (R, d, Vp)]
         if train:
-            shapes += [(V, d, R), (d, F, R), (F, d, R), (d, d, R), (3 * d, d, R), (L * 2 * d, d, B * S), (d, E, B * S),
+            shapes += [(Vp, d, R), (d, F, R), (F, d, R), (d, d, R), (3 * d, d, R), (L * 2 * d, d, B * S), (d, E, B * S),
                        (B * S, d, L * 2 * d)]
         need = max(native.gemm_workspace_bytes(m, n, k) for m, n, k in shapes)
         self.gemm_ws = torch.zeros(max(need, 4096) // 4 + 4, dtype=torch.float32, device=dev)
@@ -244,7 +256,7 @@ class DecodeState:
         e = lambda n: torch.empty(B, n, dtype=dt, device=dev)  # noqa: E731
         self.x, self.x1, self.x2, self.y, self.o, self.q = e(d), e(d), e(d), e(d), e(d), e(d)
         self.qkv, self.h = e(3 * d), e(F)
-        self.logits = torch.empty(B, V, dtype=torch.float32, device=dev)  # f32: argmax on unrounded logits
+        self.logits = torch.empty(B, padded_vocab(V), dtype=torch.float32, device=dev)  # f32: argmax on unrounded logits
 
     def token_lists(self) -> List[List[int]]:
         """Per row: START .. up to and including the first END (model.py:236-242), else max_len ids."""
@@ -269,14 +281,19 @@ class TransformerDecoder:
                  device=None, dtype: Optional[torch.dtype] = None):
         native.require_gpu()
         self.V, self.d, self.H, self.L, self.F = vocab_size, embed_dim, num_heads, num_layers, ff_dim
-        if embed_dim % num_heads or embed_dim // num_heads != 64:
-            raise ValueError(f"head_dim {embed_dim / num_heads} unsupported: the attention kernels are head_dim 64")
+        self.Vp = padded_vocab(vocab_size)
+        if embed_dim % num_heads:
+            raise ValueError(f"embed_dim {embed_dim} is not divisible by num_heads {num_heads}")
+        self.hd = embed_dim // num_heads
+        if self.hd not in (16, 32, 64, 128):
+            raise ValueError(f"head_dim {self.hd} unsupported: the attention kernels take 16, 32, 64 or 128")
         self.max_seq_len, self.dropout, self.pad_idx = max_seq_len, dropout, pad_idx
         self.embed_dim = embed_dim
         self.device = device or torch.device("cuda")
         if store is None:
             dt = dtype or torch.bfloat16
             store = FlatParams(decoder_entries(vocab_size, embed_dim, num_layers, ff_dim, None), self.device, dt)
+            store.vocab = vocab_size
             self._own_store = True
         else:
             self._own_store = False
@@ -307,11 +324,13 @@ class TransformerDecoder:
                 a = math.sqrt(6.0 / (3 * d + d))
                 t = (torch.rand(*shape, generator=g) * 2 - 1) * a
             elif len(shape) == 2:
-                fo, fi = shape
-                if name.endswith("cross_q.weight"):
-                    fo = 3 * d
+                rows, fi = shape
+                if name == "fc_out.weight":
+                    rows = self.V  # the pad rows of the head stay 0 (padded_vocab)
+                fo = 3 * d if name.endswith("cross_q.weight") else rows
                 a = math.sqrt(6.0 / (fo + fi))
-                t = (torch.rand(*shape, generator=g) * 2 - 1) * a
+                t = torch.zeros(shape)
+                t[:rows] = (torch.rand(rows, fi, generator=g) * 2 - 1) * a
             elif "norm" in name:
                 t = torch.ones(shape) if name.endswith("weight") else torch.zeros(shape)
             elif any(s in name for s in ("self_in.bias", "self_out.bias", "cross_q.bias", "cross_out.bias",
@@ -322,7 +341,9 @@ class TransformerDecoder:
                                                                                         if name.startswith("layers.")
                                                                                         else name]
                 b = 1 / math.sqrt(fan_in)
-                t = (torch.rand(*shape, generator=g) * 2 - 1) * b
+                n = self.V if name == "fc_out.bias" else shape[0]
+                t = torch.zeros(shape)
+                t[:n] = (torch.rand(n, generator=g) * 2 - 1) * b
             self.store.p(name).copy_(t)
         self.store.sync_shadow()
 
@@ -378,18 +399,18 @@ class TransformerDecoder:
             native.linear(xin, w(pre + "self_in.weight"), qkv, bias=st.p(pre + "self_in.bias"))
             sa = native.attn_args(qkv, 3 * d, T * 3 * d, qkv[:, d:], 3 * d, T * 3 * d, qkv[:, 2 * d:], 3 * d, T * 3 * d,
                                   A.os[j], d, T * d, lse=A.lse_s[j], key_tokens=tokens, tok_batch=T,
-                                  pad_idx=self.pad_idx, causal=True, scale=1.0 / math.sqrt(64), drop_p=p, seed=seed,
+                                  pad_idx=self.pad_idx, causal=True, scale=1.0 / math.sqrt(self.hd), drop_p=p, seed=seed,
                                   site=base + 0)
-            native.attention_fwd(native.dtype_code(qkv), B, H, T, T, sa)
+            native.attention_fwd(native.dtype_code(qkv), B, H, T, T, sa, Dh=self.hd)
             native.linear(A.os[j], w(pre + "self_out.weight"), A.y, bias=st.p(pre + "self_out.bias"), workspace=ws)
             native.layernorm_fwd(xin, st.p(pre + "norm1.weight"), st.p(pre + "norm1.bias"), 1e-5, xs[0], r=A.y,
                                  drop_p=p, seed=seed, site=base + 1, z=z[0], mean=stt[0][0], rstd=stt[0][1])
             native.linear(xs[0], w(pre + "cross_q.weight"), A.qc[j], bias=st.p(pre + "cross_q.bias"), workspace=ws)
             kvl = A.kv[:, l * 2 * d:]
             ca = native.attn_args(A.qc[j], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
-                                  S * L * 2 * d, A.oc[j], d, T * d, lse=A.lse_c[j], scale=1.0 / math.sqrt(64), drop_p=p,
+                                  S * L * 2 * d, A.oc[j], d, T * d, lse=A.lse_c[j], scale=1.0 / math.sqrt(self.hd), drop_p=p,
                                   seed=seed, site=base + 2)
-            native.attention_fwd(native.dtype_code(qkv), B, H, T, S, ca)
+            native.attention_fwd(native.dtype_code(qkv), B, H, T, S, ca, Dh=self.hd)
             native.linear(A.oc[j], w(pre + "cross_out.weight"), A.y, bias=st.p(pre + "cross_out.bias"), workspace=ws)
             native.layernorm_fwd(xs[0], st.p(pre + "norm2.weight"), st.p(pre + "norm2.bias"), 1e-5, xs[1], r=A.y,
                                  drop_p=p, seed=seed, site=base + 3, z=z[1], mean=stt[1][0], rstd=stt[1][1])
@@ -455,8 +476,9 @@ class TransformerDecoder:
                 side.under(lambda: grads_ready(first, last))
 
         # fc_out
-        dW(dlogits, x_last, "fc_out.weight", "fc_out.bias", V, d, R, V, d)
-        native.gemm(dlogits, w("fc_out.weight"), A.dx, R, d, V, b_layout=MN, ldb=d, workspace=ws)
+        Vp = self.Vp  # dlogits [R, Vp]: the pad columns hold exactly 0 (padded_vocab)
+        dW(dlogits, x_last, "fc_out.weight", "fc_out.bias", Vp, d, R, Vp, d)
+        native.gemm(dlogits, w("fc_out.weight"), A.dx, R, d, Vp, b_layout=MN, ldb=d, workspace=ws)
         ready("fc_out.weight", "fc_out.bias")
         ascale = 1.0 / (1.0 - p) if p > 0 else 1.0
         for l in reversed(range(L)):
@@ -483,12 +505,12 @@ class TransformerDecoder:
             native.gemm(A.dy, w(pre + "cross_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)
             kvl, dkvl = A.kv[:, l * 2 * d:], A.dkv[:, l * 2 * d:]
             ca = native.attn_args(A.qc[l], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
-                                  S * L * 2 * d, A.oc[l], d, T * d, lse=A.lse_c[l], scale=1.0 / math.sqrt(64), drop_p=p,
+                                  S * L * 2 * d, A.oc[l], d, T * d, lse=A.lse_c[l], scale=1.0 / math.sqrt(self.hd), drop_p=p,
                                   seed=seed, site=base + 2)
             cg = native.attn_grads(A.do, d, T * d, A.dq, d, T * d, dkvl, L * 2 * d, S * L * 2 * d, dkvl[:, d:],
                                    L * 2 * d, S * L * 2 * d, A.delta)
             guard(A.dq)
-            native.attention_bwd(native.dtype_code(A.dq), B, H, T, S, ca, cg)
+            native.attention_bwd(native.dtype_code(A.dq), B, H, T, S, ca, cg, Dh=self.hd)
             dW(A.dq, xs[0], pre + "cross_q.weight", pre + "cross_q.bias", d, d, R, d, d)
             native.gemm(A.dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d,
                         workspace=ws)
@@ -501,12 +523,12 @@ class TransformerDecoder:
             qkv = A.qkv[l]
             sa = native.attn_args(qkv, 3 * d, T * 3 * d, qkv[:, d:], 3 * d, T * 3 * d, qkv[:, 2 * d:], 3 * d, T * 3 * d,
                                   A.os[l], d, T * d, lse=A.lse_s[l], key_tokens=tokens, tok_batch=T,
-                                  pad_idx=self.pad_idx, causal=True, scale=1.0 / math.sqrt(64), drop_p=p, seed=seed,
+                                  pad_idx=self.pad_idx, causal=True, scale=1.0 / math.sqrt(self.hd), drop_p=p, seed=seed,
                                   site=base + 0)
             sg = native.attn_grads(A.do, d, T * d, A.dqkv, 3 * d, T * 3 * d, A.dqkv[:, d:], 3 * d, T * 3 * d,
                                    A.dqkv[:, 2 * d:], 3 * d, T * 3 * d, A.delta)
             guard(A.dqkv)
-            native.attention_bwd(native.dtype_code(A.dq), B, H, T, T, sa, sg)
+            native.attention_bwd(native.dtype_code(A.dq), B, H, T, T, sa, sg, Dh=self.hd)
             dW(A.dqkv, xin, pre + "self_in.weight", pre + "self_in.bias", 3 * d, d, R, 3 * d, d)
             native.gemm(A.dqkv, w(pre + "self_in.weight"), A.dx, R, d, 3 * d, b_layout=MN, ldb=d, residual=A.dx,
                         ldr=d, workspace=ws)
@@ -557,13 +579,13 @@ class TransformerDecoder:
             native.kv_store(stt.qkv[:, d:], 3 * d, cache, 2 * d, Tm * 2 * d, B, 2 * d, stt.pos)
             native.attention_decode(stt.qkv, 3 * d, cache, 2 * d, Tm * 2 * d, cache[:, :, d:], 2 * d, Tm * 2 * d, stt.o,
                                     d, B, H, pos=stt.pos, key_tokens=stt.ids, tok_batch=Tm, pad_idx=self.pad_idx,
-                                    scale=1.0 / math.sqrt(64))
+                                    scale=1.0 / math.sqrt(self.hd))
             native.linear(stt.o, w(pre + "self_out.weight"), stt.y, bias=st.p(pre + "self_out.bias"))
             native.layernorm_fwd(x, st.p(pre + "norm1.weight"), st.p(pre + "norm1.bias"), 1e-5, stt.x1, r=stt.y)
             native.linear(stt.x1, w(pre + "cross_q.weight"), stt.q, bias=st.p(pre + "cross_q.bias"))
             kvl = stt.kv[:, l * 2 * d:]
             native.attention_decode(stt.q, d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d, S * L * 2 * d,
-                                    stt.o, d, B, H, Lk=S, scale=1.0 / math.sqrt(64))
+                                    stt.o, d, B, H, Lk=S, scale=1.0 / math.sqrt(self.hd), Dh=self.hd)
             native.linear(stt.o, w(pre + "cross_out.weight"), stt.y, bias=st.p(pre + "cross_out.bias"))
             native.layernorm_fwd(stt.x1, st.p(pre + "norm2.weight"), st.p(pre + "norm2.bias"), 1e-5, stt.x2, r=stt.y)
             native.linear(stt.x2, w(pre + "linear1.weight"), stt.h, bias=st.p(pre + "linear1.bias"),
@@ -571,7 +593,7 @@ class TransformerDecoder:
             native.linear(stt.h, w(pre + "linear2.weight"), stt.y, bias=st.p(pre + "linear2.bias"))
             native.layernorm_fwd(stt.x2, st.p(pre + "norm3.weight"), st.p(pre + "norm3.bias"), 1e-5, x, r=stt.y)
         native.linear(x, w("fc_out.weight"), stt.logits, bias=st.p("fc_out.bias"))
-        native.greedy_pick(stt.logits, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished, stt.n_finished)
+        native.greedy_pick(stt.logits, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished, stt.n_finished, V=V)
         native.step_inc(stt.pos)
 
     def forward(self, tgt_tokens: torch.Tensor, memory: torch.Tensor, memory_padding_mask=None) -> torch.Tensor:
@@ -584,11 +606,17 @@ class TransformerDecoder:
         S = memory.shape[1]
         mem = memory.to(self.device, self.dtype).reshape(B * S, self.d).contiguous()
         A = self.acts(B, T, S, False)
-        out = torch.empty(B * T, self.V, dtype=torch.float32, device=self.device)
+        out = torch.empty(B * T, self.Vp, dtype=torch.float32, device=self.device)
         self.run_forward(tokens, mem, self.d, S, A, None, False, logits_out=out)
-        return out.view(B, T, self.V)
+        return self.unpad_logits(out, B, T)
 
     __call__ = forward
+
+    def unpad_logits(self, out: torch.Tensor, B: int, T: int) -> torch.Tensor:
+        """[B*T, Vp] head output -> [B, T, V] (a copy only when V is not a multiple of 8)."""
+        if self.Vp == self.V:
+            return out.view(B, T, self.V)
+        return out[:, :self.V].reshape(B, T, self.V)
 
     def flops_per_sequence(self, T: int, S: int) -> float:
         """Algorithmic forward FLOPs for one caption (SURVEY.md §8d convention)."""

@@ -60,8 +60,9 @@ class VisionEncoder:
         self.kind = spec["kind"]
         self.E, self.L, self.H, self.mlp = spec["hidden"], spec["layers"], spec["heads"], spec["mlp"]
         self.image, self.patch, self.eps = spec["image"], spec["patch"], spec["eps"]
-        if self.E % self.H or self.E // self.H != 64:
-            raise ValueError(f"encoder head_dim {self.E / self.H} unsupported (kernels are head_dim 64)")
+        if self.E % self.H or self.E // self.H not in (16, 32, 64, 128):
+            raise ValueError(f"encoder head_dim {self.E / self.H} unsupported (kernels take 16, 32, 64, 128)")
+        self.hd = self.E // self.H
         self.np = (self.image // self.patch) ** 2
         self.N = self.np + 1
         self.kin = 3 * self.patch * self.patch
@@ -233,8 +234,8 @@ class VisionEncoder:
             native.layernorm_fwd(h, w[f"{i}.ln1.w"], w[f"{i}.ln1.b"], self.eps, a)
             native.linear(a, w[f"{i}.qkv.w"], qkv, bias=w[f"{i}.qkv.b"])
             args = native.attn_args(qkv, 3 * E, N * 3 * E, qkv[:, E:], 3 * E, N * 3 * E, qkv[:, 2 * E:], 3 * E,
-                                    N * 3 * E, o, E, N * E, scale=1.0 / math.sqrt(64))
-            native.attention_fwd(native.dtype_code(qkv), B, H, N, N, args)
+                                    N * 3 * E, o, E, N * E, scale=1.0 / math.sqrt(self.hd))
+            native.attention_fwd(native.dtype_code(qkv), B, H, N, N, args, Dh=self.hd)
             native.linear(o, w[f"{i}.o.w"], h, bias=w[f"{i}.o.b"], residual=h)
             native.layernorm_fwd(h, w[f"{i}.ln2.w"], w[f"{i}.ln2.b"], self.eps, a)
             native.linear(a, w[f"{i}.fc1.w"], m, bias=w[f"{i}.fc1.b"], act=act)

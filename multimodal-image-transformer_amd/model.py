@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 import config
+import data
 import native
 from decoder import TransformerDecoder, decoder_entries, flat_to_reference, reference_to_flat
 from encoder import VisionEncoder, build_encoder
@@ -50,40 +51,23 @@ def _dtype_from_config(dtype):
     return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32}[dtype]
 
 
-class ViTImageProcessorLite:
-    """ViTImageProcessor defaults (tf/models/vit/image_processing_vit.py; mean = std = 0.5,
-    tf/utils/constants.py:3-4): RGB, resize to size x size with PIL bilinear, /255, (x - 0.5)/0.5.
-    Host-side preprocessing, used by generate() (model.py:192)."""
-
-    def __init__(self, size: int = 224, mean=(0.5, 0.5, 0.5), std=(0.5, 0.5, 0.5)):
-        self.size, self.mean, self.std = size, np.asarray(mean, np.float32), np.asarray(std, np.float32)
-
-    def __call__(self, images, return_tensors="pt"):
-        from PIL import Image
-        ims = images if isinstance(images, (list, tuple)) else [images]
-        out = []
-        for im in ims:
-            if not isinstance(im, Image.Image):
-                im = Image.fromarray(np.asarray(im))
-            im = im.convert("RGB").resize((self.size, self.size), Image.BILINEAR)
-            a = np.asarray(im, dtype=np.float32) / 255.0
-            a = (a - self.mean) / self.std
-            out.append(torch.from_numpy(a.transpose(2, 0, 1).copy()))
-        return {"pixel_values": torch.stack(out)}
-
-
 class GraphedStep:
     """A captured train step. step(images, decoder_input_tokens, target_tokens) copies a batch into
-    the static buffers (skip by passing nothing) and replays; returns the loss device scalar."""
+    the static buffers (skip by passing nothing) and replays; returns the loss device scalar. The
+    learning rate is a device scalar the graph reads, refreshed from optimizer.param_groups before
+    every replay (a scheduler's change takes effect like in the eager loop)."""
 
-    def __init__(self, graph, images, dec_in, targets, loss):
+    def __init__(self, graph, images, dec_in, targets, loss, optimizer=None):
         self.graph, self.images, self.dec_in, self.targets, self.loss = graph, images, dec_in, targets, loss
+        self.optimizer = optimizer
 
     def __call__(self, images=None, decoder_input_tokens=None, target_tokens=None):
         if images is not None:
             self.images.copy_(images, non_blocking=True)
             self.dec_in.copy_(decoder_input_tokens, non_blocking=True)
             self.targets.copy_(target_tokens, non_blocking=True)
+        if self.optimizer is not None:
+            self.optimizer._sync_lr()
         self.graph.replay()
         return self.loss
 
@@ -112,6 +96,7 @@ class ImageToTextModel:
         self.has_projection = E != d  # model.py:97-102: Linear if dims differ, else Identity
         self.store = FlatParams(decoder_entries(decoder_vocab_size, d, decoder_layers, decoder_ff_dim,
                                                 E if self.has_projection else None), self.device, self.dtype)
+        self.store.vocab = decoder_vocab_size
         self.decoder = TransformerDecoder(decoder_vocab_size, d, decoder_heads, decoder_layers, decoder_ff_dim,
                                           decoder_max_seq_len, decoder_dropout, decoder_pad_idx, store=self.store,
                                           device=self.device)
@@ -122,7 +107,10 @@ class ImageToTextModel:
             self.store.p("projection.weight").copy_((torch.rand(d, E, generator=g) * 2 - 1) * b)
             self.store.p("projection.bias").copy_((torch.rand(d, generator=g) * 2 - 1) * b)
             self.store.sync_shadow()
-        self.image_processor = ViTImageProcessorLite(self.encoder.image)
+        # the processor the encoder was trained with (model.py:69-83 loads AutoImageProcessor for the
+        # encoder's name): ViT = bilinear resize + mean/std 0.5; CLIP = shortest-edge bicubic resize,
+        # centre crop, CLIP mean/std — bit-identical to the HF processors (tests/test_data_*.py)
+        self.image_processor = data.ImagePreprocessor(self.encoder.kind, self.encoder.image, self.device)
         self.training = True
         # dropout RNG state: a device counter (graph-replay safe), distinct per DP rank
         self.seed_t = torch.tensor([seed * 1000003], dtype=torch.int64, device=self.device)
@@ -217,12 +205,12 @@ class ImageToTextModel:
         B, T = tokens.shape
         mem, mem_ld, S, _, _ = self._encode_memory(images)
         A = self.decoder.acts(B, T, S, False)
-        out = torch.empty(B * T, self.decoder.V, dtype=torch.float32, device=self.device)
+        out = torch.empty(B * T, self.decoder.Vp, dtype=torch.float32, device=self.device)
         p = self.decoder.dropout if self.training else 0.0
         if p > 0:
             native.step_inc(self.seed_t)
         self.decoder.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, False, logits_out=out, drop_p=p)
-        return out.view(B, T, self.decoder.V)
+        return self.decoder.unpad_logits(out, B, T)
 
     __call__ = forward
 
@@ -267,7 +255,8 @@ class ImageToTextModel:
         native.count_targets(targets, self.decoder_pad_idx, A.count)
         if dist is not None:
             dist.all_reduce_count(A.count)
-        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, True, row_loss=A.row_loss)
+        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, True, row_loss=A.row_loss,
+                             V=dec.V, ld=dec.Vp)
         proj = (enc_rows, enc_ld, self.encoder_output_dim) if self.has_projection else None
         dec.run_backward(tokens, mem, mem_ld, S, A, self.seed_t, logits, proj_input=proj,
                          grads_ready=dist.grads_ready if dist is not None else None)
@@ -305,7 +294,7 @@ class ImageToTextModel:
         with torch.cuda.graph(graph):
             loss = self.train_step(st_img, st_in, st_tg)
             optimizer.step(max_norm)
-        return GraphedStep(graph, st_img, st_in, st_tg, loss)
+        return GraphedStep(graph, st_img, st_in, st_tg, loss, optimizer)
 
     @torch.no_grad()
     def eval_loss(self, images, decoder_input_tokens, target_tokens) -> torch.Tensor:
@@ -320,7 +309,8 @@ class ImageToTextModel:
         native.zero(A.count)
         native.zero(A.loss_sum)
         native.count_targets(targets, self.decoder_pad_idx, A.count)
-        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, False, row_loss=A.row_loss)
+        native.cross_entropy(logits, targets, self.decoder_pad_idx, A.count, A.loss_sum, False, row_loss=A.row_loss,
+                             V=self.decoder.V, ld=self.decoder.Vp)
         native.scalar_div(A.loss_sum, A.count, A.loss)
         return A.loss
 
@@ -412,7 +402,15 @@ class ImageToTextModel:
         with torch.no_grad():
             for k, v in flat.items():
                 if k in names:
-                    self.store.p(k).copy_(v.to(self.device, torch.float32).reshape(self.store.p(k).shape))
+                    dst = self.store.p(k)
+                    v = v.to(self.device, torch.float32)
+                    if k.startswith("fc_out.") and v.shape[0] != dst.shape[0]:  # padded vocabulary head
+                        if v.shape[0] != self.decoder.V:
+                            raise ValueError(f"{k}: {tuple(v.shape)} does not match vocab {self.decoder.V}")
+                        dst.zero_()
+                        dst[:v.shape[0]].copy_(v)
+                    else:
+                        dst.copy_(v.reshape(dst.shape))
         self.store.sync_shadow()
         return self
 

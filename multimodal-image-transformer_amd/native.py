@@ -88,7 +88,7 @@ SIGNATURES = {
     "mit_zero": (I, [vp, L, vp]),
     "mit_scalar_div": (I, [vp, vp, vp, vp]),
     "mit_dropout_mask": (I, [L, Fl, vp, U32, vp, vp]),
-    "mit_attention_decode": (I, [I, L, L, vp, L, vp, L, L, vp, L, L, vp, L, L, vp, vp, L, I, Fl, vp]),
+    "mit_attention_decode": (I, [I, L, L, L, vp, L, vp, L, L, vp, L, L, vp, L, L, vp, vp, L, I, Fl, vp]),
     "mit_kv_store": (I, [I, L, L, vp, L, vp, L, L, vp, vp]),
     "mit_embed_decode": (I, [I, L, L, vp, L, vp, vp, Fl, vp, vp, vp]),
     "mit_image_normalize": (I, [L, L, L, vp, vp, ctypes.POINTER(Fl), ctypes.POINTER(Fl), vp]),
@@ -430,9 +430,9 @@ def dropout_mask(n, p, seed, site, out):
 
 # --- batched greedy decoding (decode.hip) -------------------------------------------------------
 def attention_decode(q, q_batch, k, k_row, k_batch, v, v_row, v_batch, o, o_batch, B, H, *, Lk=0, pos=None,
-                     key_tokens=None, tok_batch=0, pad_idx=0, scale=0.125):
+                     key_tokens=None, tok_batch=0, pad_idx=0, scale=0.125, Dh=64):
     """One query per (b, h) over Lk keys (Lk = pos+1 from the device scalar when pos is given)."""
-    _check(lib().mit_attention_decode(dtype_code(q), B, H, ptr(q), q_batch, ptr(k), k_row, k_batch, ptr(v), v_row,
+    _check(lib().mit_attention_decode(dtype_code(q), B, H, Dh, ptr(q), q_batch, ptr(k), k_row, k_batch, ptr(v), v_row,
                                       v_batch, ptr(o), o_batch, Lk, ptr(pos), ptr(key_tokens), tok_batch, pad_idx,
                                       scale, stream_ptr()), "mit_attention_decode")
 
@@ -448,8 +448,9 @@ def embed_decode(ids, pos, table, scale, pe, out):
                                   ptr(pe), ptr(out), stream_ptr()), "mit_embed_decode")
 
 
-def greedy_pick(logits, ids, pos, end_id, pad_id, finished, n_finished):
-    B, V = logits.shape
+def greedy_pick(logits, ids, pos, end_id, pad_id, finished, n_finished, V=None):
+    B = logits.shape[0]
+    V = V if V is not None else logits.shape[1]
     _check(lib().mit_greedy_pick(B, V, ptr(logits), logits.stride(0), ptr(ids), ids.shape[1], ptr(pos), int(end_id),
                                  int(pad_id), ptr(finished), ptr(n_finished), stream_ptr()), "mit_greedy_pick")
 

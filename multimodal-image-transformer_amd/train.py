@@ -48,8 +48,7 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
         for b in it:
             b = dict(b)
             if b["images"].dtype == torch.uint8:
-                pre = pre or data.ImagePreprocessor.for_encoder(device=model.device)
-                b["images"] = pre.normalize(b["images"])
+                b["images"] = model.image_processor.normalize(b["images"])
             else:
                 b["images"] = b["images"].to(model.device, non_blocking=True)
             yield b
@@ -89,8 +88,7 @@ def evaluate(model, dataloader, criterion, device):
     for batch in dataloader:
         images = batch["images"]
         if images.dtype == torch.uint8:  # data.collate_fn batches: normalised on the GPU
-            pre = pre or data.ImagePreprocessor.for_encoder(device=model.device)
-            images = pre.normalize(images)
+            images = model.image_processor.normalize(images)
         total += model.eval_loss(images, batch["decoder_input_tokens"], batch["target_tokens"])
         n += 1
     model.train()

@@ -13,8 +13,12 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 sys.path.insert(0, GOLDEN)
 import procedural as P  # noqa: E402
 
+# every BASELINE config is pinned by one of these: configs[0] = cfg0_b4_* (d128 / 8 heads = head_dim 16),
+# configs[1] = cfg1_b2_patches, configs[2] = cfg2_b2_patches (CLIP-L/14@336, S = 577),
+# configs[3] = cfg3_b2_patches (+ dp2_tiny for the data-parallel step), configs[4] = cfg1_gen_cls;
+# tiny_vit_v509 has a vocabulary that is not a multiple of 8
 CASES = ["tiny_vit_cls", "tiny_vit_patches", "tiny_clip336_patches", "tiny_clip336_cls", "cfg1_b2_patches",
-         "cfg3_b2_patches"]
+         "cfg3_b2_patches", "cfg0_b4_cls", "cfg0_b4_patches", "cfg2_b2_patches", "tiny_vit_v509"]
 
 
 @lru_cache(maxsize=None)
@@ -60,6 +64,23 @@ def inputs(meta, step: int = 0):
     cap = P.make_captions(meta["B"], meta["cap_len"], meta["dec"]["vocab"], meta["seed"] + 2 + step,
                           meta["lengths"])
     return imgs, cap[:, :-1].contiguous(), cap[:, 1:].contiguous()
+
+
+def logits_at(meta, T, logits):
+    """The reference logits a fixture pins and ours at the same places: full [B,T,V], or the
+    row-sampled positions ("fwd.logits_sel", meta["logit_sel"] = [[b, t], ...])."""
+    if "fwd.logits" in T:
+        return logits, T["fwd.logits"]
+    sel = meta["logit_sel"]
+    got = torch.stack([logits[b, t] for b, t in sel])
+    return got, T["fwd.logits_sel"]
+
+
+def encoder_rows(T, feats):
+    """(ours, reference) pairs for the encoder's last_hidden_state entries a fixture holds."""
+    if "enc.last_hidden_state" in T:
+        return [(feats, T["enc.last_hidden_state"])]
+    return [(feats[:, 0], T["enc.cls_rows"]), (feats[:, 17], T["enc.row17"]), (feats[:, -1], T["enc.row_last"])]
 
 
 def trainable_names(meta):

@@ -148,17 +148,25 @@ def run_case(name, enc_kind, enc_cfg, dec, mode, *, B, cap_len, lengths, seed, i
     with torch.no_grad():
         lhs = m.encoder(pixel_values=images).last_hidden_state
         logits = m(images, batches[0]["decoder_input_tokens"])
-    if lhs.numel() <= 1_200_000:
+    if lhs.numel() <= 600_000:
         out["enc.last_hidden_state"] = lhs.contiguous()
     else:
         out["enc.cls_rows"] = lhs[:, 0, :].contiguous()
         out["enc.row17"] = lhs[:, 17, :].contiguous()
         out["enc.row_last"] = lhs[:, -1, :].contiguous()
+    logit_sel = None
     if full_logits:
         out["fwd.logits"] = logits.contiguous()
     else:
         out["fwd.logits_pos0"] = logits[:, 0, :].contiguous()
         out["fwd.logits_poslast"] = logits[:, -1, :].contiguous()
+        # row-sampled logits: 8 positions per caption (first, last, 6 seeded) pin the whole sequence
+        Tt = logits.shape[1]
+        logit_sel = []
+        for b in range(B):
+            extra = P.sample_index(Tt - 2, 6, seed + 300 + b) + 1
+            logit_sel += [[b, t] for t in sorted({0, Tt - 1, *extra.tolist()})]
+        out["fwd.logits_sel"] = torch.stack([logits[b, t] for b, t in logit_sel]).contiguous()
     out["fwd.argmax"] = logits.argmax(-1).to(torch.float32)
     top2 = logits.topk(2, dim=-1).values
     out["fwd.margin"] = (top2[..., 0] - top2[..., 1]).contiguous()
@@ -220,7 +228,7 @@ def run_case(name, enc_kind, enc_cfg, dec, mode, *, B, cap_len, lengths, seed, i
         "weights_checksum": P.checksum(state[n] for n, _ in spec),
         "images_checksum": P.checksum([images]),
         "captions_checksum": P.checksum(caps),
-        "sample_index": meta_idx, "generate": gen_meta,
+        "sample_index": meta_idx, "generate": gen_meta, "logit_sel": logit_sel,
         "versions": {"torch": torch.__version__, "transformers": __import__("transformers").__version__},
     }
     path = os.path.join(HERE, f"{name}.safetensors")
@@ -259,6 +267,46 @@ def run_dp_case(name, enc_kind, enc_cfg, dec, *, B, cap_len, lengths, seed, imag
     print(f"{name}: {os.path.getsize(path)/1e6:.2f} MB loss={avg:.5f}", flush=True)
 
 
+class _TensorProcessor:
+    """Stands in for the HF image processor when generate() is handed an already-normalised tensor
+    (the reference's generate calls self.image_processor(images=..., return_tensors="pt"), model.py:192)."""
+
+    class _Out(dict):
+        def to(self, device):
+            return self
+
+    def __call__(self, images, return_tensors="pt"):
+        return self._Out(pixel_values=images)
+
+
+def run_gen_case(name, enc_kind, enc_cfg, dec, *, n_images, seed, image_size, max_len, start, end):
+    """Reference greedy generate (model.py:171-242, cls memory as the reference computes it) on
+    procedural images with the initial procedural weights (configs[4]: batched decode parity)."""
+    torch.manual_seed(0)
+    m, spec, state = build_reference(enc_kind, enc_cfg, dec, "cls", seed)
+    m.image_processor = _TensorProcessor()
+    images = P.make_images(n_images, image_size, seed + 7)
+    ids = [ref_model.ImageToTextModel.generate(m, images[i:i + 1], start_token_id=start, end_token_id=end,
+                                               max_len=max_len) for i in range(n_images)]
+    # the full teacher-forced logits of each generated sequence: argmax margins for near-tie handling
+    margins = []
+    with torch.no_grad():
+        for i, row in enumerate(ids):
+            lg = m(images[i:i + 1], torch.tensor([row[:-1]]))[0]
+            top2 = lg.topk(2, dim=-1).values
+            margins.append((top2[:, 0] - top2[:, 1]).tolist())
+    meta = {"case": name, "enc_kind": enc_kind, "enc_cfg": enc_cfg, "dec": dec, "mode": "cls", "seed": seed,
+            "image_size": image_size, "n_images": n_images, "image_seed": seed + 7, "max_len": max_len,
+            "start": start, "end": end, "ids": ids, "margins": margins,
+            "spec": [[n, list(s)] for n, s in spec], "weights_checksum": P.checksum(state[n] for n, _ in spec),
+            "images_checksum": P.checksum([images]),
+            "versions": {"torch": torch.__version__, "transformers": __import__("transformers").__version__}}
+    path = os.path.join(HERE, f"{name}.safetensors")
+    save_file({"ids_flat": torch.tensor([t for r in ids for t in r], dtype=torch.float32)}, path,
+              metadata={"meta": json.dumps(meta)})
+    print(f"{name}: {[len(r) for r in ids]} ids, min margin {min(min(x) for x in margins):.4f}", flush=True)
+
+
 TINY_VIT = dict(hidden_size=128, num_hidden_layers=2, num_attention_heads=2, intermediate_size=512,
                 image_size=224, patch_size=16)
 TINY_CLIP = dict(hidden_size=128, num_hidden_layers=2, num_attention_heads=2, intermediate_size=512,
@@ -267,6 +315,13 @@ TINY_DEC = dict(vocab=512, embed_dim=128, heads=2, layers=2, ff=512)
 # decoder width differs from the encoder width so the projection is a real Linear (model.py:97-99)
 TINY_DEC96 = dict(vocab=512, embed_dim=192, heads=3, layers=2, ff=384)
 CFG1_DEC = dict(vocab=10000, embed_dim=512, heads=8, layers=6, ff=2048)
+# configs[0]: 2L d128 decoder with 8 heads (head_dim 16), ff = 4d
+CFG0_DEC = dict(vocab=10000, embed_dim=128, heads=8, layers=2, ff=512)
+# configs[2]: CLIP ViT-L/14@336 (577 tokens) + the cfg1 decoder
+CLIP_L14_336 = dict(hidden_size=1024, intermediate_size=4096, num_hidden_layers=24, num_attention_heads=16,
+                    image_size=336, patch_size=14)
+# a vocabulary that is not a multiple of 8 (the tokenizer decides V, tokenizer.py:200-201)
+TINY_DEC509 = dict(vocab=509, embed_dim=192, heads=3, layers=2, ff=384)
 # configs[3]: CLIP ViT-L/14 (224 px -> 257 tokens) + 12L d768 decoder (H = 12, ff = 4d)
 CLIP_L14 = dict(hidden_size=1024, intermediate_size=4096, num_hidden_layers=24, num_attention_heads=16,
                 image_size=224, patch_size=14)
@@ -298,6 +353,22 @@ if __name__ == "__main__":
     if want("cfg3_b2_patches"):
         run_case("cfg3_b2_patches", "clip", CLIP_L14, CFG3_DEC, "patches", B=2, cap_len=64, lengths=[64, 37],
                  seed=41, image_size=224, steps=1, full_logits=False)
+    if want("cfg0_b4_cls"):
+        run_case("cfg0_b4_cls", "vit", {}, CFG0_DEC, "cls", B=4, cap_len=32, lengths=[32, 29, 20, 11],
+                 seed=51, image_size=224, full_logits=False)
+    if want("cfg0_b4_patches"):
+        run_case("cfg0_b4_patches", "vit", {}, CFG0_DEC, "patches", B=4, cap_len=32, lengths=[32, 30, 17, 6],
+                 seed=52, image_size=224, full_logits=False)
+    if want("cfg2_b2_patches"):
+        run_case("cfg2_b2_patches", "clip", CLIP_L14_336, CFG1_DEC, "patches", B=2, cap_len=64, lengths=[64, 45],
+                 seed=61, image_size=336, steps=1, full_logits=False)
+    if want("tiny_vit_v509"):
+        run_case("tiny_vit_v509", "vit", TINY_VIT, TINY_DEC509, "patches", B=4, cap_len=24, lengths=[24, 19, 12, 5],
+                 seed=71, image_size=224)
+    if want("cfg1_gen_cls"):
+        # configs[4] parity anchor: the cfg1 architecture with the cfg1_b2_patches weights (seed 21)
+        run_gen_case("cfg1_gen_cls", "vit", {}, CFG1_DEC, n_images=4, seed=21, image_size=224, max_len=16,
+                     start=ref_config.START_TOKEN_ID, end=ref_config.END_TOKEN_ID)
     if want("dp2_tiny"):
         run_dp_case("dp2_tiny", "vit", TINY_VIT, TINY_DEC96, B=8, cap_len=20,
                     lengths=[20, 20, 18, 20, 7, 9, 11, 5], seed=31, image_size=224)

@@ -21,9 +21,9 @@ def _gpu():
     N.load_library()
 
 
-def _ref_attn(q, k, v, lk, key_tokens=None, pad=0):
-    """q [B,H,64], k/v [B,Lmax,H,64] -> o [B,H,64] over keys < lk, PAD keys masked (float64)."""
-    s = torch.einsum("bhd,bjhd->bhj", q.double(), k[:, :lk].double()) / 8.0
+def _ref_attn(q, k, v, lk, key_tokens=None, pad=0, scale=0.125):
+    """q [B,H,hd], k/v [B,Lmax,H,hd] -> o [B,H,hd] over keys < lk, PAD keys masked (float64)."""
+    s = torch.einsum("bhd,bjhd->bhj", q.double(), k[:, :lk].double()) * scale
     if key_tokens is not None:
         s = s.masked_fill((key_tokens[:, :lk] == pad)[:, None, :], float("-inf"))
     p = torch.softmax(s, -1)
@@ -31,9 +31,11 @@ def _ref_attn(q, k, v, lk, key_tokens=None, pad=0):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("lk", [1, 7, 33, 64, 197])
-def test_attention_decode_self_with_pad(dtype, lk):
-    B, H, Lmax, d = 5, 8, 200, 512
+@pytest.mark.parametrize("lk,hd", [(1, 64), (7, 64), (33, 64), (64, 64), (197, 64), (33, 16), (197, 16), (33, 32),
+                                   (64, 128)])
+def test_attention_decode_self_with_pad(dtype, lk, hd):
+    B, Lmax, d = 5, 200, 512
+    H = d // hd
     g = torch.Generator().manual_seed(lk)
     dev = torch.device("cuda")
     qkv = torch.randn(B, 3 * d, generator=g).to(dev, dtype)
@@ -45,11 +47,11 @@ def test_attention_decode_self_with_pad(dtype, lk):
     pos = torch.tensor([lk - 1], dtype=torch.int64, device=dev)
     o = torch.empty(B, d, device=dev, dtype=dtype)
     N.attention_decode(qkv, 3 * d, cache, 2 * d, Lmax * 2 * d, cache[:, :, d:], 2 * d, Lmax * 2 * d, o, d, B, H,
-                       pos=pos, key_tokens=toks_d, tok_batch=Lmax, pad_idx=0)
-    q = qkv[:, :d].view(B, H, 64).cpu()
-    k = cache[:, :, :d].reshape(B, Lmax, H, 64).cpu()
-    v = cache[:, :, d:].reshape(B, Lmax, H, 64).cpu()
-    ref = _ref_attn(q, k, v, lk, toks, 0).view(B, d)
+                       pos=pos, key_tokens=toks_d, tok_batch=Lmax, pad_idx=0, scale=hd ** -0.5, Dh=hd)
+    q = qkv[:, :d].view(B, H, hd).cpu()
+    k = cache[:, :, :d].reshape(B, Lmax, H, hd).cpu()
+    v = cache[:, :, d:].reshape(B, Lmax, H, hd).cpu()
+    ref = _ref_attn(q, k, v, lk, toks, 0, scale=hd ** -0.5).view(B, d)
     got = o.double().cpu()
     # rows whose keys are all PAD (lk == 1: rows 0 and 1) are NaN, like the reference's softmax
     dead = torch.isnan(ref).any(-1)
@@ -165,3 +167,64 @@ def test_generate_captions_postprocessed_like_reference():
         want = inference.postprocess_ids(ref, g["start"], g["end"])
         assert ids == want
         assert text == " ".join(f"t{i}" for i in want)
+
+
+def _cfg1_gen_model(dtype):
+    meta, _ = FX.load("cfg1_gen_cls")
+    m, _ = build_model(meta, dtype)
+    return meta, m
+
+
+def _gen_images(meta, B):
+    """The fixture's 4 images first, then B-4 more procedural ones."""
+    import procedural as P
+    imgs = P.make_images(meta["n_images"], meta["image_size"], meta["image_seed"])
+    rest = P.make_images(B - meta["n_images"], meta["image_size"], meta["image_seed"] + 1000)
+    return torch.cat([imgs, rest])
+
+
+def test_generate_batch_b256_cfg1_matches_reference_ids():
+    """configs[4] at its size: 256 images through the cfg1 architecture (ViT-B/16 + 6L d512,
+    V = 10000), decoded to max_len 100 with an END that is never produced (every row runs all 99
+    token steps). The first 4 images' ids equal the reference generate() (model.py:171-242) on the
+    same weights/images (fixture cfg1_gen_cls, max_len 16) — fp32 mode, so ties are not an issue."""
+    meta, m = _cfg1_gen_model(torch.float32)
+    images = _gen_images(meta, 256).cuda()
+    ids = m.generate_batch(images, meta["start"], -1, max_len=100)
+    assert len(ids) == 256 and all(len(r) == 100 for r in ids)
+    for i in range(meta["n_images"]):
+        ref = meta["ids"][i]
+        assert ids[i][:len(ref)] == ref, (i, ids[i][:len(ref)], ref)
+
+
+def test_generate_batch_b256_bf16_agrees_with_full_forward():
+    """bf16 batched KV-cache decode (the configs[4] benchmark path) at B = 256, max_len 100: every
+    generated token equals the argmax of the teacher-forced full forward (model.forward, the
+    reference's recompute path) on the generated prefix, up to each row's first bf16 near-tie (top-1 -
+    top-2 margin < 3e-2 of the full forward's logits; random-init weights give many: the reference's
+    own 4 images have margins down to 2.7e-3), after which the two paths see different prefixes."""
+    meta, m = _cfg1_gen_model(torch.bfloat16)
+    images = _gen_images(meta, 256).cuda()
+    ids = torch.tensor(m.generate_batch(images, meta["start"], -1, max_len=100))
+    with torch.no_grad():
+        logits = m(images, ids[:, :-1].cuda())  # [256, 99, V] f32
+        top2 = logits.topk(2, dim=-1)
+        am = top2.indices[..., 0].cpu()
+        margin = (top2.values[..., 0] - top2.values[..., 1]).cpu()
+    del logits
+    nxt = ids[:, 1:]
+    # after a disagreement the two paths see different prefixes: compare up to each row's first
+    # near-tie position
+    bad = 0
+    tied = 0
+    for b in range(256):
+        for t in range(99):
+            if am[b, t] != nxt[b, t]:
+                if margin[b, t] < 3e-2:
+                    tied += 1
+                    break
+                bad += 1
+                break
+    print(f"b256 bf16 decode: {tied} rows stopped at a near-tie, {bad} real disagreements")
+    assert bad == 0
+    assert tied <= 256 // 4

@@ -1,0 +1,104 @@
+"""The data-parallel train step through the REAL HIP path: two ranks (gloo; RCCL needs one GPU per
+rank, the box has one) share cuda:0 and run ImageToTextModel.train_step(dist=DataParallel) on the two
+halves of the dp2_tiny batch — the HIP backward announces its gradient buckets (grads_ready) from
+the weight-gradient side stream, DataParallel all-reduces them and the global non-PAD count.
+The summed gradients, the loss and the AdamW update must equal the reference's single-process
+step at the global batch (tests/golden/dp2_tiny: train.py:62-123 at B = 8, unequal PAD per half)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import fixtures as FX
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(here, "..", "multimodal-image-transformer_amd"), os.path.join(here, "golden")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import fixtures as FX
+        import optim
+        from dist import DataParallel
+        from model_util import build_model
+        import procedural as P
+        meta, T = FX.load("dp2_tiny")
+        m, _ = build_model(meta, torch.float32)
+        m.train()
+        dp = DataParallel(m, overlap=True)
+        imgs = P.make_images(meta["B"], meta["image_size"], meta["seed"] + 1)
+        cap = P.make_captions(meta["B"], meta["cap_len"], meta["dec"]["vocab"], meta["seed"] + 2, meta["lengths"])
+        half = meta["B"] // world
+        sl = slice(rank * half, (rank + 1) * half)
+        opt = optim.AdamW(m.store, lr=meta["lr"], betas=tuple(meta["betas"]), eps=meta["eps"],
+                          weight_decay=meta["weight_decay"])
+        before = m.state_dict()
+        loss = m.train_step(imgs[sl].cuda(), cap[sl, :-1].cuda(), cap[sl, 1:].cuda(), dist=dp)
+        torch.cuda.synchronize()
+        grad = m.store.grad.clone().cpu()
+        opt.step(meta["clip"])
+        torch.cuda.synchronize()
+        after = m.state_dict()
+        if rank == 0:
+            names = FX.trainable_names(meta)
+            # numpy (pickled by value): the worker may exit before the parent reads the queue
+            q.put((loss.item(), grad.numpy(), opt.norm_t.cpu().tolist(),
+                   {k: (after[k] - before[k]).cpu().numpy() for k in names}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp2_train_step_on_hip_path_matches_reference():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    meta, T = FX.load("dp2_tiny")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    loss, grad, (total, coef), deltas = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert abs(loss - T["loss"].item()) < 1e-4
+    assert abs(total - T["grad_total_norm_preclip"].item()) < 1e-3 * total
+    from decoder import decoder_entries, flat_to_reference
+    from params import FlatParams
+    dec, enc = FX.dec_desc(meta), FX.enc_desc(meta)
+    E = enc["hidden"]
+    store = FlatParams(decoder_entries(dec["vocab"], dec["d"], dec["layers"], dec["ff"],
+                                       E if E != dec["d"] else None), torch.device("cpu"), torch.float32)
+    store.grad.copy_(torch.from_numpy(grad))
+    deltas = {k: torch.from_numpy(v) for k, v in deltas.items()}
+
+    class GV:
+        vocab = dec["vocab"]
+
+        def p(self, n):
+            return store.g(n)
+
+    named = flat_to_reference(GV(), dec["layers"], dec["d"])
+    if "projection.weight" in store.index:
+        named["projection.weight"] = store.g("projection.weight")
+        named["projection.bias"] = store.g("projection.bias")
+    for k in FX.trainable_names(meta):
+        FX.compare_stat("grad1", k, named[k] * coef, T, meta, rtol=2e-3, atol=2e-6, scale_tol=1e-3, outlier_frac=2e-3)
+        FX.compare_stat("delta1", k, deltas[k], T, meta, rtol=2e-3, atol=2e-6)

@@ -172,11 +172,16 @@ def _attn_ref(q, k, v, causal, kpm, scale, drop=None):
     return p @ v, lse
 
 
+_HD_CASES = [(64, k) for k in ["self_causal_pad", "cross", "bidir", "cross_s1", "self_drop", "self_long", "cross577",
+                                "cross_drop", "bidir577"]]
+# other head dims (generic kernels): configs[0]'s decoder is d128 / 8 heads = head_dim 16
+_HD_CASES += [(hd, k) for hd in (16, 32, 128) for k in ["self_causal_pad", "cross", "self_drop", "cross_s1"]]
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("kind", ["self_causal_pad", "cross", "bidir", "cross_s1", "self_drop", "self_long",
-                                  "cross577", "cross_drop", "bidir577"])
-def test_attention_fwd_bwd(dtype, kind):
-    B, H, D = 3, 4, 64
+@pytest.mark.parametrize("D,kind", _HD_CASES)
+def test_attention_fwd_bwd(dtype, D, kind):
+    B, H = 3, 4
     if kind == "self_causal_pad" or kind == "self_drop":
         Lq = Lk = 63
     elif kind in ("cross", "cross_drop"):
@@ -207,9 +212,9 @@ def test_attention_fwd_bwd(dtype, kind):
     lse = torch.empty(B * H * Lq, device=dev())
     seed = torch.tensor([99], dtype=torch.int64, device=dev())
     args = N.attn_args(q, H * D, Lq * H * D, k, 2 * H * D, Lk * 2 * H * D, v, 2 * H * D, Lk * 2 * H * D, o, H * D,
-                       Lq * H * D, lse=lse, key_tokens=tok, tok_batch=Lk, pad_idx=0, causal=causal, scale=0.125,
-                       drop_p=drop_p, seed=seed, site=5)
-    N.attention_fwd(N.dtype_code(q), B, H, Lq, Lk, args)
+                       Lq * H * D, lse=lse, key_tokens=tok, tok_batch=Lk, pad_idx=0, causal=causal,
+                       scale=D ** -0.5, drop_p=drop_p, seed=seed, site=5)
+    N.attention_fwd(N.dtype_code(q), B, H, Lq, Lk, args, Dh=D)
     qh = q.float().view(B, Lq, H, D).transpose(1, 2).requires_grad_(True)
     kh = k.float().reshape(B, Lk, H, D).transpose(1, 2).requires_grad_(True)
     vh = v.float().reshape(B, Lk, H, D).transpose(1, 2).requires_grad_(True)
@@ -218,7 +223,7 @@ def test_attention_fwd_bwd(dtype, kind):
         mk = torch.empty(B * H * Lq * Lk, device=dev())
         N.dropout_mask(mk.numel(), drop_p, seed, 5, mk)
         drop = mk.view(B, H, Lq, Lk)
-    oref, lref = _attn_ref(qh, kh, vh, causal, kpm, 0.125, drop)
+    oref, lref = _attn_ref(qh, kh, vh, causal, kpm, D ** -0.5, drop)
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
     _close(o.view(B, Lq, H, D).transpose(1, 2), oref, tol)
     _close(lse.view(B, H, Lq), lref, 1e-3 if dtype == torch.bfloat16 else 1e-5)
@@ -229,7 +234,7 @@ def test_attention_fwd_bwd(dtype, kind):
     delta = torch.empty(B * H * Lq, device=dev())
     grads = N.attn_grads(do, H * D, Lq * H * D, dq, H * D, Lq * H * D, dkv[..., :H * D], 2 * H * D, Lk * 2 * H * D,
                          dkv[..., H * D:], 2 * H * D, Lk * 2 * H * D, delta)
-    N.attention_bwd(N.dtype_code(q), B, H, Lq, Lk, args, grads)
+    N.attention_bwd(N.dtype_code(q), B, H, Lq, Lk, args, grads, Dh=D)
     gt = 4e-2 if dtype == torch.bfloat16 else 2e-4
     _close(dq.view(B, Lq, H, D).transpose(1, 2), qh.grad, gt)
     _close(dkv[..., :H * D].reshape(B, Lk, H, D).transpose(1, 2), kh.grad, gt)

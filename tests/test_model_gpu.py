@@ -35,12 +35,8 @@ def test_forward_fp32_matches_reference(name):
     meta, T = FX.load(name)
     m, _ = build_model(meta, torch.float32)
     logits, tg = _fwd(m, meta)
-    if "fwd.logits" in T:
-        ref = T["fwd.logits"]
-        torch.testing.assert_close(logits, ref, rtol=0, atol=1e-3)
-    else:
-        torch.testing.assert_close(logits[:, 0], T["fwd.logits_pos0"], rtol=0, atol=1e-3)
-        torch.testing.assert_close(logits[:, -1], T["fwd.logits_poslast"], rtol=0, atol=1e-3)
+    got, ref = FX.logits_at(meta, T, logits)
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-3)
     safe = T["fwd.margin"] > 1e-4
     assert torch.equal(logits.argmax(-1).float()[safe], T["fwd.argmax"][safe])
     loss = torch.nn.functional.cross_entropy(logits.reshape(-1, logits.shape[-1]), tg.reshape(-1), ignore_index=0)
@@ -52,9 +48,7 @@ def test_forward_bf16_matches_reference(name):
     meta, T = FX.load(name)
     m, _ = build_model(meta, torch.bfloat16)
     logits, tg = _fwd(m, meta)
-    key = "fwd.logits" if "fwd.logits" in T else "fwd.logits_pos0"
-    got = logits if key == "fwd.logits" else logits[:, 0]
-    ref = T[key]
+    got, ref = FX.logits_at(meta, T, logits)
     # north star: logits within 1e-2 in bf16 — relative L2 error <= 1e-2, and no element off by
     # more than 2e-2 of the logit scale (bf16 keeps 8 mantissa bits: ~4e-3 per rounding)
     rel = ((got - ref).norm() / ref.norm()).item()
@@ -68,10 +62,27 @@ def test_forward_bf16_matches_reference(name):
     assert agree == 1.0, f"argmax agreement {agree:.4f} on margin>5e-2 positions"
 
 
-def _grad_ref_name_map(m):
-    """flat entry -> reference name (for non-split params) used to compare gradients."""
-    from decoder import flat_to_reference
-    return flat_to_reference
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("name", CASES)
+def test_encoder_matches_reference(name, dtype):
+    """The frozen encoder's last_hidden_state (HF ViT / CLIP vision tower) against the reference's,
+    directly (not only through the decoder): fp32 within 1e-3; bf16 relative L2 <= 1.5e-2 and max
+    error <= 3e-2 of the row scale (bf16 keeps 8 mantissa bits and the residual stream is bf16: the
+    measured rel-L2 is 5.6e-3 for 2 layers, 9.1e-3 for ViT-B/16's 12, 1.07e-2 for CLIP-L's 24 —
+    DESIGN.md §6)."""
+    meta, T = FX.load(name)
+    m, _ = build_model(meta, dtype)
+    imgs, _, _ = FX.inputs(meta, 0)
+    with torch.no_grad():
+        feats = m.encoder.forward(imgs.cuda(), rows="all").float().cpu()
+    for got, ref in FX.encoder_rows(T, feats):
+        if dtype == torch.float32:
+            torch.testing.assert_close(got, ref, rtol=0, atol=1e-3)
+        else:
+            rel = ((got - ref).norm() / ref.norm()).item()
+            err = (got - ref).abs().max().item()
+            print(f"{name}: bf16 encoder rows rel-L2 {rel:.2e} max abs {err:.3e} (scale {ref.abs().max():.2f})")
+            assert rel <= 1.5e-2 and err <= 3e-2 * ref.abs().max().item()
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -122,6 +133,7 @@ class _GradView:
 
     def __init__(self, store):
         self.s = store
+        self.vocab = getattr(store, "vocab", None)
 
     def p(self, name):
         return self.s.g(name)

@@ -21,17 +21,11 @@ def test_oracle_forward_matches_reference(name):
     meta, T, st, enc, dec, imgs, dec_in, tgt = _run_oracle_case(name)
     with torch.no_grad():
         feats = R.encode(st, imgs, enc)
-        if "enc.last_hidden_state" in T:
-            torch.testing.assert_close(feats, T["enc.last_hidden_state"], rtol=1e-4, atol=1e-4)
-        else:
-            torch.testing.assert_close(feats[:, 0], T["enc.cls_rows"], rtol=1e-4, atol=1e-4)
-            torch.testing.assert_close(feats[:, 17], T["enc.row17"], rtol=1e-4, atol=1e-4)
+        for got, ref in FX.encoder_rows(T, feats):
+            torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
         logits = R.model_forward(st, imgs, dec_in, enc, dec, meta["mode"])
-    if "fwd.logits" in T:
-        torch.testing.assert_close(logits, T["fwd.logits"], rtol=1e-4, atol=1e-4)
-    else:
-        torch.testing.assert_close(logits[:, 0], T["fwd.logits_pos0"], rtol=1e-4, atol=1e-4)
-        torch.testing.assert_close(logits[:, -1], T["fwd.logits_poslast"], rtol=1e-4, atol=1e-4)
+    got, ref = FX.logits_at(meta, T, logits)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
     am = logits.argmax(-1).float()
     safe = T["fwd.margin"] > 1e-4
     assert torch.equal(am[safe], T["fwd.argmax"][safe])
@@ -86,6 +80,20 @@ def test_oracle_generate_matches_reference():
         torch.testing.assert_close(pv, T[f"gen.pixel_values{k}"], rtol=0, atol=1e-5)
         ids = R.greedy_generate(st, pv, enc, dec, g["start"], g["end"], g["max_len"], meta["mode"])
         assert ids == g["ids"][k]
+
+
+def test_oracle_batched_generate_fixture():
+    """cfg1_gen_cls (configs[4] anchor): the oracle's greedy ids = the reference's on all 4 images."""
+    import procedural as P
+    meta, _ = FX.load("cfg1_gen_cls")
+    st = FX.state(meta)
+    enc, dec = FX.enc_desc(meta), FX.dec_desc(meta)
+    imgs = P.make_images(meta["n_images"], meta["image_size"], meta["image_seed"])
+    assert abs(P.checksum([imgs]) - meta["images_checksum"]) < 1e-6 * abs(meta["images_checksum"])
+    torch.set_num_threads(8)
+    for i in range(meta["n_images"]):
+        ids = R.greedy_generate(st, imgs[i:i + 1], enc, dec, meta["start"], meta["end"], meta["max_len"], "cls")
+        assert ids == meta["ids"][i]
 
 
 def test_procedural_inputs_stable():
