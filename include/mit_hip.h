@@ -187,10 +187,15 @@ int mit_vit_assemble(int dtype, long B, long np, long E, const void* patch, cons
  * table in the operand dtype [V, d]; pe f32 [>=T, d]. */
 int mit_embed_fwd(int dtype, long B, long T, long d, const int64_t* tokens, const void* table, float scale,
                   const float* pe, float drop_p, const uint64_t* seed, uint32_t site, void* out, void* stream);
-/* dtable[tok] += scale * dropout_mask * dx (f32, atomics; caller zeroes dtable); the padding_idx
- * row receives no gradient (nn.Embedding(padding_idx=PAD), decoder.py:105). */
+/* dtable[tok] += scale * dropout_mask * dx (f32; caller zeroes dtable); the padding_idx row receives
+ * no gradient (nn.Embedding(padding_idx=PAD), decoder.py:105; embedding backward of autograd).
+ * plan != NULL: DETERMINISTIC — each token's row is the sum of its positions' rows in a fixed order
+ * (d <= 1024); plan = int32 [mit_embed_plan_ints(B*T)] filled by mit_embed_plan from the same tokens
+ * (any time after the tokens are final). plan == NULL: float atomics (order-dependent rounding). */
+long mit_embed_plan_ints(long n);
+int mit_embed_plan(const int64_t* tokens, long n, int* plan, void* stream);
 int mit_embed_bwd(int dtype, long B, long T, long d, const int64_t* tokens, const void* dx, float scale, float drop_p,
-                  const uint64_t* seed, uint32_t site, int pad_idx, float* dtable, void* stream);
+                  const uint64_t* seed, uint32_t site, int pad_idx, const int* plan, float* dtable, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Cross-entropy with ignore_index (train.py:90,327 -> torch/nn/functional.py cross_entropy).

@@ -117,6 +117,81 @@ __global__ void embed_bwd_kernel(long B, long T_, long d, const int64_t* __restr
   }
 }
 
+// Deterministic embedding backward (replaces the float atomics above): the gradient row of token v
+// is the sum over the positions holding v, taken in a FIXED order. Plan (depends on the tokens
+// only): rank_i = #{j: tok_j < tok_i} + #{j < i: tok_j == tok_i} is position i's slot in the
+// (token, position)-sorted order; plan[rank_i] = i, and the first position of every token records
+// its segment length and start. One 64-thread block per 64 positions, tokens staged in LDS tiles.
+__global__ __launch_bounds__(64) void embed_plan_kernel(const int64_t* __restrict__ tok, int n, int* __restrict__ plan) {
+  __shared__ int64_t ts[64];
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  const int64_t ti = i < n ? tok[i] : 0;
+  int less = 0, eq_before = 0, eq = 0;
+  for (int j0 = 0; j0 < n; j0 += 64) {
+    __syncthreads();
+    if (j0 + (int)threadIdx.x < n) ts[threadIdx.x] = tok[j0 + threadIdx.x];
+    __syncthreads();
+    const int nj = min(64, n - j0);
+    for (int jj = 0; jj < nj; ++jj) {
+      const int64_t t = ts[jj];
+      const int e = t == ti;
+      less += t < ti;
+      eq += e;
+      eq_before += e & (j0 + jj < i);
+    }
+  }
+  if (i < n) {
+    const int rank = less + eq_before;
+    plan[rank] = i;
+    plan[n + i] = eq_before == 0 ? eq : 0;  // segment head: its length, else 0
+    plan[2 * n + i] = rank;                 // segment start (sorted slot of the head)
+  }
+}
+
+// one block per position; the head of each token's segment sums the segment's dx rows: wave w takes
+// rows w, w+4, ... in sorted (= position) order, the 4 wave partials are added in wave order, and the
+// row is STORED (dtable is zeroed once before; PAD's row receives nothing). d <= 1024.
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_seg_kernel(int n, int d, const int64_t* __restrict__ tok,
+                                                            const T* __restrict__ dx, float scale,
+                                                            const uint64_t* seed, uint32_t site, uint32_t thresh,
+                                                            float dscale, int dropout, int pad,
+                                                            const int* __restrict__ plan, float* __restrict__ dtable) {
+  __shared__ float part[4][1024];
+  const int i = blockIdx.x;
+  const int len = plan[n + i];
+  if (len == 0) return;
+  const int64_t id = tok[i];
+  if (id == pad) return;
+  const int* perm = plan + plan[2 * n + i];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t key = dropout ? site_key(seed, site) : 0ull;
+  float acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  for (int k = w; k < len; k += 4) {
+    const long j = perm[k];
+    const T* row = dx + j * d;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = lane + 64 * q;
+      if (c < d) {
+        float g = to_f(row[c]) * scale;
+        if (dropout) g *= drop_mul(key, (uint64_t)(j * d + c), thresh, dscale);
+        acc[q] += g;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int c = lane + 64 * q;
+    if (c < d) part[w][c] = acc[q];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < d; c += 256)
+    dtable[id * d + c] = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
+}
+
 // ---------------------------------------------------------------------------------------------
 // cross entropy (one 256-thread block per row), in-place gradient
 // ---------------------------------------------------------------------------------------------
@@ -424,14 +499,34 @@ extern "C" int mit_embed_fwd(int dtype, long B, long T_, long d, const int64_t* 
   return MIT_OK;
 }
 
+extern "C" long mit_embed_plan_ints(long n) { return 3 * n; }
+
+extern "C" int mit_embed_plan(const int64_t* tokens, long n, int* plan, void* stream) {
+  MIT_CHECK_ARG(tokens && plan && n >= 0 && n < (1L << 30), "mit_embed_plan: bad arguments");
+  if (n == 0) return MIT_OK;
+  hipLaunchKernelGGL(embed_plan_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, tokens,
+                     (int)n, plan);
+  MIT_LAUNCH_CHECK("mit_embed_plan");
+  return MIT_OK;
+}
+
 extern "C" int mit_embed_bwd(int dtype, long B, long T_, long d, const int64_t* tokens, const void* dx, float scale,
-                             float drop_p, const uint64_t* seed, uint32_t site, int pad_idx, float* dtable,
-                             void* stream) {
+                             float drop_p, const uint64_t* seed, uint32_t site, int pad_idx, const int* plan,
+                             float* dtable, void* stream) {
   MIT_CHECK_ARG(tokens && dx && dtable, "mit_embed_bwd: null pointer");
   const long total = B * T_ * d;
   const int dropout = drop_p > 0.f;
   const uint32_t th = drop_threshold(drop_p);
   const float sc = drop_p < 1.f ? 1.f / (1.f - drop_p) : 0.f;
+  if (plan) {
+    MIT_CHECK_ARG(d <= 1024 && B * T_ < (1L << 30), "mit_embed_bwd: the deterministic path takes d <= 1024");
+    if (B * T_ == 0) return MIT_OK;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_seg_kernel<T>, dim3((unsigned)(B * T_)), dim3(256), 0,
+                                         (hipStream_t)stream, (int)(B * T_), (int)d, tokens, (const T*)dx, scale, seed,
+                                         site, th, sc, dropout, pad_idx, plan, dtable));
+    MIT_LAUNCH_CHECK("mit_embed_bwd");
+    return MIT_OK;
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_kernel<T>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                                        B, T_, d, tokens, (const T*)dx, scale, seed, site, th, sc, dropout, pad_idx,
                                        dtable));

@@ -189,6 +189,8 @@ class _Acts:
             # one column-partial buffer per LayerNorm: their dgamma/dbeta reductions run on the
             # side stream, off the dX chain (run_backward)
             self.ln_ws_side = [f(native.layernorm_bwd_ws_floats(R, d)) for _ in range(3 * L)]
+            # deterministic embedding-gradient order (native.embed_plan of the step's tokens)
+            self.emb_plan = torch.empty(native.embed_plan_ints(R), dtype=torch.int32, device=dev)
             # the weight-gradient GEMMs run on a side stream (_SideStream) with their own scratch
             self.gemm_ws_side = torch.zeros(max(need, 4096) // 4 + 4, dtype=torch.float32, device=dev)
 
@@ -205,6 +207,7 @@ class _SideStream:
         self.stream = torch.cuda.Stream(device=device, priority=priority)
         self.ptr = self.stream.cuda_stream
         self.events = native.HipEvents(64)  # recorded on the main stream (side waits for main)
+        self.plan_events = native.HipEvents(2)  # the embedding plan (side) -> embedding backward (main)
         self.side_events = native.HipEvents(128)  # recorded on the side stream only: a recycled slot
         self.pending = {}                         # re-recorded later on the SAME stream stays a safe wait
 
@@ -440,6 +443,13 @@ class TransformerDecoder:
         x_last = A.xs[L - 1][2]
         ws = A.gemm_ws
         side = self._side_stream() if self.dw_side_stream else None
+        # the embedding gradient's deterministic summation order depends on the tokens only: build it
+        # on the side stream now, off the dX chain
+        if side is None:
+            native.embed_plan(tokens, A.emb_plan)
+        else:
+            side.run(lambda: native.embed_plan(tokens, A.emb_plan))
+            plan_ev = side.plan_events.record(side.ptr)
 
         def dW(dy, x, wname, bname, M, N, K, lda, ldb):
             """weight grad dY^T X (TN GEMM) with the bias grad (row sums of dY^T) fused in, split-K;
@@ -539,7 +549,10 @@ class TransformerDecoder:
         # embedding (scatter-add into a zeroed table gradient; PAD row gets nothing)
         ge = g("token_embedding.weight")
         native.zero(ge)
-        native.embed_bwd(tokens, A.dx, math.sqrt(d), ge, self.pad_idx, drop_p=p, seed=seed, site=EMB_SITE)
+        if side is not None:
+            native.HipEvents.wait(native.stream_ptr(), plan_ev)
+        native.embed_bwd(tokens, A.dx, math.sqrt(d), ge, self.pad_idx, drop_p=p, seed=seed, site=EMB_SITE,
+                         plan=A.emb_plan)
         last = "token_embedding.weight"
         if proj_input is not None:
             enc_rows, enc_ld, E = proj_input

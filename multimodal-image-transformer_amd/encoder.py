@@ -76,48 +76,80 @@ class VisionEncoder:
     def hidden_size(self):
         return self.E
 
-    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor]):
-        """Load HF ViTModel / CLIPVisionModel weights (any of the naming schemes above)."""
-        n = {_normalize_hf_key(k): v.detach().float().cpu() for k, v in sd.items()}
-        E, dt, dev = self.E, self.dtype, self.device
+    # tensors the reference model holds but last_hidden_state never reads (ViTModel's pooler,
+    # modeling_vit.py:386; CLIPVisionTransformer's post_layernorm, modeling_clip.py:649): kept as
+    # host copies so state_dict() round-trips and the parameter count matches the reference's
+    def _extra_shapes(self):
+        E = self.E
+        if self.kind == "vit":
+            return {"pooler.dense.weight": (E, E), "pooler.dense.bias": (E,)}
+        return {"post_layernorm.weight": (E,), "post_layernorm.bias": (E,)}
 
-        def get(k):
+    def num_reference_params(self) -> int:
+        """len(list(encoder.parameters())) of the reference's HF module: patch/cls/pos (+ CLIP's
+        pre_layrnorm), 16 per layer, ViT's final LayerNorm, and the extras above."""
+        if self.kind == "vit":
+            return 4 + 16 * self.L + 2 + 2
+        return 3 + 2 + 16 * self.L + 2
+
+    def _collect(self, sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """HF-named state -> this encoder's host tensors; raises KeyError / ValueError (nothing is
+        modified) when a tensor is missing or has the wrong shape."""
+        n = {_normalize_hf_key(k): v.detach().float().cpu() for k, v in sd.items()}
+        E, mlp = self.E, self.mlp
+
+        def get(k, shape):
             if k not in n:
                 raise KeyError(f"encoder weight '{k}' missing (have e.g. {sorted(n)[:4]})")
-            return n[k]
+            t = n[k]
+            if t.numel() != int(torch.tensor(shape).prod()):
+                raise ValueError(f"encoder weight '{k}': {tuple(t.shape)} does not fit {shape}")
+            return t.reshape(shape)
 
         w = {}
         if self.kind == "vit":
-            pw = get("embeddings.patch_embeddings.projection.weight").reshape(E, -1)
-            pb = get("embeddings.patch_embeddings.projection.bias")
-            cls = get("embeddings.cls_token").reshape(E)
-            pos = get("embeddings.position_embeddings").reshape(self.N, E)
+            pw = get("embeddings.patch_embeddings.projection.weight", (E, self.kin))
+            pb = get("embeddings.patch_embeddings.projection.bias", (E,))
+            cls = get("embeddings.cls_token", (E,))
+            pos = get("embeddings.position_embeddings", (self.N, E))
         else:
-            pw = get("embeddings.patch_embedding.weight").reshape(E, -1)
+            pw = get("embeddings.patch_embedding.weight", (E, self.kin))
             pb = torch.zeros(E)
-            cls = get("embeddings.class_embedding").reshape(E)
-            pos = get("embeddings.position_embedding.weight").reshape(self.N, E)
-            w["pre_ln.w"] = get("pre_layrnorm.weight")
-            w["pre_ln.b"] = get("pre_layrnorm.bias")
+            cls = get("embeddings.class_embedding", (E,))
+            pos = get("embeddings.position_embedding.weight", (self.N, E))
+            w["pre_ln.w"] = get("pre_layrnorm.weight", (E,))
+            w["pre_ln.b"] = get("pre_layrnorm.bias", (E,))
         pwp = torch.zeros(E, self.kpad)
         pwp[:, :self.kin] = pw
         w["patch.w"], w["patch.b"], w["cls"], w["pos"] = pwp, pb, cls, pos
         for i in range(self.L):
             p = f"layers.{i}."
-            w[f"{i}.ln1.w"], w[f"{i}.ln1.b"] = get(p + "layernorm_before.weight"), get(p + "layernorm_before.bias")
-            w[f"{i}.ln2.w"], w[f"{i}.ln2.b"] = get(p + "layernorm_after.weight"), get(p + "layernorm_after.bias")
-            w[f"{i}.qkv.w"] = torch.cat([get(p + f"attention.{x}_proj.weight") for x in "qkv"], 0)
-            w[f"{i}.qkv.b"] = torch.cat([get(p + f"attention.{x}_proj.bias") for x in "qkv"], 0)
-            w[f"{i}.o.w"], w[f"{i}.o.b"] = get(p + "attention.o_proj.weight"), get(p + "attention.o_proj.bias")
-            w[f"{i}.fc1.w"], w[f"{i}.fc1.b"] = get(p + "mlp.fc1.weight"), get(p + "mlp.fc1.bias")
-            w[f"{i}.fc2.w"], w[f"{i}.fc2.b"] = get(p + "mlp.fc2.weight"), get(p + "mlp.fc2.bias")
+            w[f"{i}.ln1.w"], w[f"{i}.ln1.b"] = get(p + "layernorm_before.weight", (E,)), get(p + "layernorm_before.bias", (E,))
+            w[f"{i}.ln2.w"], w[f"{i}.ln2.b"] = get(p + "layernorm_after.weight", (E,)), get(p + "layernorm_after.bias", (E,))
+            w[f"{i}.qkv.w"] = torch.cat([get(p + f"attention.{x}_proj.weight", (E, E)) for x in "qkv"], 0)
+            w[f"{i}.qkv.b"] = torch.cat([get(p + f"attention.{x}_proj.bias", (E,)) for x in "qkv"], 0)
+            w[f"{i}.o.w"], w[f"{i}.o.b"] = get(p + "attention.o_proj.weight", (E, E)), get(p + "attention.o_proj.bias", (E,))
+            w[f"{i}.fc1.w"], w[f"{i}.fc1.b"] = get(p + "mlp.fc1.weight", (mlp, E)), get(p + "mlp.fc1.bias", (mlp,))
+            w[f"{i}.fc2.w"], w[f"{i}.fc2.b"] = get(p + "mlp.fc2.weight", (E, mlp)), get(p + "mlp.fc2.bias", (E,))
         if self.kind == "vit":
-            w["final_ln.w"], w["final_ln.b"] = get("layernorm.weight"), get("layernorm.bias")
+            w["final_ln.w"], w["final_ln.b"] = get("layernorm.weight", (E,)), get("layernorm.bias", (E,))
+        extra = {k: get(k, shp).clone() for k, shp in self._extra_shapes().items() if k in n}
+        return w, extra
+
+    def check_hf_state_dict(self, sd: Dict[str, torch.Tensor]):
+        self._collect(sd)
+
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor]):
+        """Load HF ViTModel / CLIPVisionModel weights (any of the naming schemes above)."""
+        w, extra = self._collect(sd)
+        dt, dev = self.dtype, self.device
         out = {}
         for k, v in w.items():
             is_mat = k.endswith(".w") and v.dim() == 2 and not k.endswith("ln.w")
             out[k] = v.to(device=dev, dtype=dt if is_mat else torch.float32).contiguous()
         self.w = out
+        old = getattr(self, "extra", {})
+        self.extra = {k: extra.get(k, old.get(k, torch.zeros(shp))) for k, shp in self._extra_shapes().items()}
         return self
 
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:
@@ -152,6 +184,8 @@ class VisionEncoder:
             sd[p + "mlp.fc2.weight"], sd[p + "mlp.fc2.bias"] = w[f"{i}.fc2.w"], w[f"{i}.fc2.b"]
         if self.kind == "vit":
             sd["layernorm.weight"], sd["layernorm.bias"] = w["final_ln.w"], w["final_ln.b"]
+        for k, v in getattr(self, "extra", {}).items():
+            sd[k] = v.clone()
         return sd
 
     def random_init(self, seed: int = 0):
@@ -170,12 +204,16 @@ class VisionEncoder:
             sd["embeddings.position_embeddings"] = rnd(1, self.N, E, scale=0.02)
             sd["layernorm.weight"] = 1 + rnd(E, scale=0.02)
             sd["layernorm.bias"] = rnd(E, scale=0.02)
+            sd["pooler.dense.weight"] = rnd(E, E, scale=0.02)
+            sd["pooler.dense.bias"] = torch.zeros(E)
         else:
             sd["embeddings.patch_embedding.weight"] = rnd(E, 3, self.patch, self.patch, scale=self.kin ** -0.5)
             sd["embeddings.class_embedding"] = rnd(E, scale=0.02)
             sd["embeddings.position_embedding.weight"] = rnd(self.N, E, scale=0.02)
             sd["pre_layrnorm.weight"] = 1 + rnd(E, scale=0.02)
             sd["pre_layrnorm.bias"] = rnd(E, scale=0.02)
+            sd["post_layernorm.weight"] = torch.ones(E)
+            sd["post_layernorm.bias"] = torch.zeros(E)
         for i in range(self.L):
             p = f"layers.{i}."
             for x in "qkvo":

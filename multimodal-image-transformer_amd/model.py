@@ -19,9 +19,9 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Dict, List, Optional
+from collections import OrderedDict
+from typing import Dict, Iterator, List, Optional, Tuple
 
-import numpy as np
 import torch
 
 import config
@@ -72,6 +72,29 @@ class GraphedStep:
         return self.loss
 
 
+class _ModelFunction(torch.autograd.Function):
+    """``logits = model(images, tokens)`` with autograd, for the reference loop shape
+    (train.py:80-100: criterion(logits) -> loss.backward() -> clip_grad_norm_(model.parameters())
+    -> optimizer.step()). forward runs the HIP forward keeping every layer's activations in the
+    training arena; backward runs the HIP backward (decoder.run_backward) and hands the gradients
+    to the parameters as views of the flat gradient buffer. ``anchor`` is one trainable parameter:
+    it makes autograd record the node; no gradient flows through it (the gradients are attached to
+    every parameter directly)."""
+
+    @staticmethod
+    def forward(ctx, anchor, model, images, tokens):
+        out, state = model._forward_for_autograd(images, tokens)
+        ctx.model, ctx.state = model, state
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dlogits):
+        ctx.model._backward_for_autograd(dlogits, ctx.state)
+        ctx.state = None
+        return None, None, None, None
+
+
 class ImageToTextModel:
     def __init__(self, decoder_vocab_size: int, decoder_embed_dim: int, decoder_heads: int, decoder_layers: int,
                  decoder_ff_dim: int, decoder_max_seq_len: int, decoder_dropout: float, decoder_pad_idx: int, *,
@@ -97,6 +120,11 @@ class ImageToTextModel:
         self.store = FlatParams(decoder_entries(decoder_vocab_size, d, decoder_layers, decoder_ff_dim,
                                                 E if self.has_projection else None), self.device, self.dtype)
         self.store.vocab = decoder_vocab_size
+        # what optim.AdamW needs to speak torch.optim.AdamW's state_dict in the reference's parameter
+        # order (frozen encoder tensors first: model.py:48-66 registers the encoder before the rest)
+        self.store.layout = dict(V=decoder_vocab_size, d=d, L=decoder_layers, F=decoder_ff_dim,
+                                 proj_in=E if self.has_projection else None,
+                                 n_encoder_params=self.encoder.num_reference_params())
         self.decoder = TransformerDecoder(decoder_vocab_size, d, decoder_heads, decoder_layers, decoder_ff_dim,
                                           decoder_max_seq_len, decoder_dropout, decoder_pad_idx, store=self.store,
                                           device=self.device)
@@ -120,6 +148,8 @@ class ImageToTextModel:
         self._prefetched = None
         self._last_pf = None
         self._hi_stream = None
+        self._params: Optional["OrderedDict[str, torch.nn.Parameter]"] = None
+        self._gen = 0  # bumped by every forward that writes the shared arenas (autograd staleness check)
 
     # --- nn.Module-like surface ----------------------------------------------------------------
     def train(self, mode: bool = True):
@@ -135,8 +165,33 @@ class ImageToTextModel:
             raise ValueError("ImageToTextModel lives on the GPU it was built on")
         return self
 
-    def parameters(self):
-        return [self.store.master]
+    def _param_table(self) -> "OrderedDict[str, torch.nn.Parameter]":
+        """One nn.Parameter per trainable flat entry, ALIASING the f32 master buffer (same storage
+        and version counter): torch.optim.AdamW / clip_grad_norm_ update and read the very memory
+        the kernels use; .grad is a view of the flat gradient buffer once a backward ran."""
+        if self._params is None:
+            self._params = OrderedDict((n, torch.nn.Parameter(self.store.p(n), requires_grad=True))
+                                       for n in self.store.names())
+            for p in self._params.values():
+                p._mit_store = self.store  # optim.AdamW(model.parameters()) finds the flat buffers
+        return self._params
+
+    def parameters(self, recurse: bool = True) -> Iterator[torch.nn.Parameter]:
+        """The trainable parameters (projection + decoder; the encoder is frozen, model.py:87-90)
+        in flat-buffer order. Padded entries (the vocabulary head, decoder.padded_vocab) include
+        their zero pad rows, which get exactly-zero gradients."""
+        return iter(self._param_table().values())
+
+    def named_parameters(self, prefix: str = "", recurse: bool = True) -> Iterator[Tuple[str, torch.nn.Parameter]]:
+        for n, p in self._param_table().items():
+            yield prefix + n, p
+
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self._param_table().values():
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
 
     def num_trainable(self) -> int:
         return sum(n for _, _, _, n in self.store.entries)
@@ -182,6 +237,8 @@ class ImageToTextModel:
         encoder features that feed the projection (for its weight gradient)."""
         B = images.shape[0]
         E, d = self.encoder.E, self.decoder_embed_dim
+        self.store.ensure_shadow()
+        self._gen += 1
         pf, self._prefetched = self._prefetched, None
         if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
             _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
@@ -200,6 +257,12 @@ class ImageToTextModel:
 
     # --- forward (model.py:116-169) ------------------------------------------------------------
     def forward(self, image_tensors: torch.Tensor, tgt_tokens: torch.Tensor) -> torch.Tensor:
+        """f32 logits [B, T, V]. With grad enabled and trainable parameters, the result carries an
+        autograd node whose backward runs the HIP backward (the reference's loss.backward(),
+        train.py:93); otherwise a forward-only launch sequence."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self._param_table().values()):
+            anchor = next(iter(self._param_table().values()))
+            return _ModelFunction.apply(anchor, self, image_tensors, tgt_tokens)
         images = image_tensors.to(self.device)
         tokens = tgt_tokens.to(self.device, torch.int64).contiguous()
         B, T = tokens.shape
@@ -213,6 +276,60 @@ class ImageToTextModel:
         return self.decoder.unpad_logits(out, B, T)
 
     __call__ = forward
+
+    def _forward_for_autograd(self, image_tensors, tgt_tokens):
+        images = image_tensors.to(self.device)
+        tokens = tgt_tokens.to(self.device, torch.int64).contiguous()
+        B, T = tokens.shape
+        mem, mem_ld, S, enc_rows, enc_ld = self._encode_memory(images)
+        dec = self.decoder
+        A = dec.acts(B, T, S, True)
+        p = dec.dropout if self.training else 0.0
+        if p > 0:
+            native.step_inc(self.seed_t)
+        out = torch.empty(B * T, dec.Vp, dtype=torch.float32, device=self.device)
+        dec.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, True, logits_out=out, drop_p=p)
+        proj = (enc_rows, enc_ld, self.encoder_output_dim) if self.has_projection else None
+        return dec.unpad_logits(out, B, T), (self._gen, tokens, mem, mem_ld, S, A, proj)
+
+    def _backward_for_autograd(self, dlogits: torch.Tensor, state):
+        gen, tokens, mem, mem_ld, S, A, proj = state
+        if gen != self._gen:
+            raise RuntimeError("ImageToTextModel: backward() after a later forward — the model keeps ONE step's "
+                               "activations (HBM arenas reused every step); call backward before the next forward")
+        dec, st = self.decoder, self.store
+        R, V, Vp = tokens.numel(), dec.V, dec.Vp
+        dl = A.logits  # compute-dtype [R, Vp] gradient of the head output; pad columns exactly 0
+        g = dlogits.reshape(R, V)
+        if Vp == V and dl.dtype != torch.float32:
+            native.cast_f32(g.contiguous(), dl)
+        else:
+            if Vp != V:
+                dl[:, V:].zero_()
+            dl[:, :V].copy_(g)
+        params = self._param_table()
+        # autograd accumulates into existing .grad: keep the previous values of the parameters whose
+        # .grad already is our view (zero_grad(set_to_none=False) or a second backward)
+        views = {n: p.grad is not None and p.grad.data_ptr() == st.g(n).data_ptr() for n, p in params.items()}
+        prev = None
+        if any(views.values()):
+            prev = st.grad.clone()
+            for n, is_view in views.items():
+                if not is_view:
+                    _, off, cnt = st.index[n]
+                    prev[off:off + cnt].zero_()
+        # the dropout masks are regenerated from the seed the forward used (seed_t is unchanged:
+        # no forward ran in between, checked above)
+        dec.run_backward(tokens, mem, mem_ld, S, A, self.seed_t, dl, proj_input=proj)
+        if prev is not None:
+            st.grad.add_(prev)
+        for n, p in params.items():
+            if not p.requires_grad or views[n]:
+                continue
+            if p.grad is None:
+                p.grad = st.g(n)
+            else:
+                p.grad.add_(st.g(n))
 
     # --- fused train step (train.py:75-93) -----------------------------------------------------
     def train_step(self, images: torch.Tensor, decoder_input_tokens: torch.Tensor, target_tokens: torch.Tensor,
@@ -390,15 +507,29 @@ class ImageToTextModel:
         sd["decoder.positional_encoding.pe"] = self.decoder.pe.unsqueeze(0).clone()
         return sd
 
+    def check_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        """Raise (KeyError / ValueError) unless sd loads into this model: every trainable tensor
+        present (strict) with the reference shape, encoder keys (if any) loadable. Touches nothing."""
+        from optim import reference_trainable
+        ref_shapes = dict(reference_trainable(self.store.layout))
+        missing = [k for k in ref_shapes if k not in sd]
+        if strict and missing:
+            raise KeyError(f"missing keys: {missing[:6]}{'...' if len(missing) > 6 else ''}")
+        bad = [(k, tuple(sd[k].shape), s) for k, s in ref_shapes.items() if k in sd and tuple(sd[k].shape) != s]
+        if bad:
+            raise ValueError("shape mismatch (checkpoint vs model): " +
+                             ", ".join(f"{k} {a} vs {b}" for k, a, b in bad[:4]))
+        enc = {k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")}
+        if enc:
+            self.encoder.check_hf_state_dict(enc)
+
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        self.check_state_dict(sd, strict)
         enc = {k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")}
         if enc:
             self.encoder.load_hf_state_dict(enc)
         flat = reference_to_flat(sd, self.decoder.L, self.decoder_embed_dim)
         names = set(self.store.names())
-        missing = sorted(names - set(flat))
-        if strict and missing:
-            raise KeyError(f"missing keys for: {missing[:6]}{'...' if len(missing) > 6 else ''}")
         with torch.no_grad():
             for k, v in flat.items():
                 if k in names:

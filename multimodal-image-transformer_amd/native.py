@@ -75,7 +75,9 @@ SIGNATURES = {
     "mit_im2col": (I, [I, L, L, L, L, L, vp, vp, L, vp]),
     "mit_vit_assemble": (I, [I, L, L, L, vp, vp, vp, vp, vp]),
     "mit_embed_fwd": (I, [I, L, L, L, vp, vp, Fl, vp, Fl, vp, U32, vp, vp]),
-    "mit_embed_bwd": (I, [I, L, L, L, vp, vp, Fl, Fl, vp, U32, I, vp, vp]),
+    "mit_embed_bwd": (I, [I, L, L, L, vp, vp, Fl, Fl, vp, U32, I, vp, vp, vp]),
+    "mit_embed_plan_ints": (L, [L]),
+    "mit_embed_plan": (I, [vp, L, vp, vp]),
     "mit_count_targets": (I, [vp, L, I, vp, vp]),
     "mit_cross_entropy": (I, [I, L, L, vp, L, vp, I, vp, vp, I, vp, vp]),
     "mit_colsum": (I, [I, L, L, vp, L, vp, I, vp, vp]),
@@ -361,11 +363,21 @@ def embed_fwd(tokens, table, scale, pe, out, *, drop_p=0.0, seed=None, site=0):
                                site, ptr(out), stream_ptr()), "mit_embed_fwd")
 
 
-def embed_bwd(tokens, dx, scale, dtable, pad_idx, *, drop_p=0.0, seed=None, site=0):
+def embed_plan_ints(n):
+    return lib().mit_embed_plan_ints(n)
+
+
+def embed_plan(tokens, plan):
+    """plan (int32 [embed_plan_ints(tokens.numel())]) <- the deterministic scatter order of tokens."""
+    _check(lib().mit_embed_plan(ptr(tokens), tokens.numel(), ptr(plan), stream_ptr()), "mit_embed_plan")
+
+
+def embed_bwd(tokens, dx, scale, dtable, pad_idx, *, drop_p=0.0, seed=None, site=0, plan=None):
+    """plan from embed_plan(tokens): deterministic; None: float atomics."""
     B, T = tokens.shape
     d = dtable.shape[1]
     _check(lib().mit_embed_bwd(dtype_code(dx), B, T, d, ptr(tokens), ptr(dx), scale, drop_p, ptr(seed), site,
-                               pad_idx, ptr(dtable), stream_ptr()), "mit_embed_bwd")
+                               pad_idx, ptr(plan), ptr(dtable), stream_ptr()), "mit_embed_bwd")
 
 
 def count_targets(targets, ignore_index, count):

@@ -38,6 +38,7 @@ class FlatParams:
             self.shadow = torch.zeros(self.numel, dtype=compute_dtype, device=device)
         self.exp_avg = None
         self.exp_avg_sq = None
+        self._synced = self.master._version
 
     # views (cached: the buffers are allocated once and only ever updated in place) -------------
     def _view(self, buf, name, cache):
@@ -72,6 +73,15 @@ class FlatParams:
         """master -> bf16 shadow (after a load / manual edit; AdamW keeps them in sync itself)."""
         if self.shadow is not self.master:
             native.cast_f32(self.master, self.shadow)
+        self._synced = self.master._version
+
+    def ensure_shadow(self):
+        """Refresh the bf16 shadow if the f32 master was modified by torch since the last sync: an
+        in-place update through a parameter view (torch.optim.AdamW.step, p.data.copy_, ...) bumps
+        the version counter the views share with the master. The fused optim.AdamW writes master
+        and shadow in one kernel (no version bump, nothing to do)."""
+        if self.shadow is not self.master and self.master._version != self._synced:
+            self.sync_shadow()
 
     def zero_grad(self):
         native.zero(self.grad)

@@ -1,14 +1,15 @@
-"""Training loop surface of the reference train.py, on the fused MI355X train step.
+"""Training loop surface of the reference train.py, on the MI355X train step.
 
 ``train_one_epoch`` / ``evaluate`` keep the reference signatures (train.py:62, 125) and semantics:
-per batch zero_grad -> forward -> CE(ignore PAD) -> backward -> clip_grad_norm_(grad_clip_value)
--> optimizer.step() -> scheduler.step(); the epoch returns the mean batch loss. Differences that
-are deliberate:
-  * forward + loss + backward are ONE kernel sequence (model.train_step) and clip + AdamW one more
-    (optim.AdamW.step); ``criterion`` is accepted for signature compatibility — the loss is
-    always CrossEntropyLoss(ignore_index=PAD) as train.py:327 constructs it;
-  * the per-batch loss stays on the device; the reference's per-step ``loss.item()`` sync
-    (train.py:109) becomes one sync per ``log_interval`` batches and one at the end of the epoch.
+per batch zero_grad -> forward -> criterion -> backward -> clip_grad_norm_(grad_clip_value)
+-> optimizer.step() -> scheduler.step(); the epoch returns the mean batch loss. Two ways to run it:
+  * the fused path (optim.AdamW + the reference criterion, train.py:319-327): forward + CE +
+    backward are ONE kernel sequence (model.train_step) and clip + AdamW one more
+    (optim.AdamW.step); the per-batch loss stays on the device and the reference's per-step
+    ``loss.item()`` sync (train.py:109) becomes one sync per ``log_interval`` batches;
+  * any other optimizer / criterion (torch.optim.AdamW(model.parameters()), label smoothing, ...):
+    the reference's own call sequence through autograd (model.forward's backward is the HIP
+    backward).
 ``main()`` runs the loop on synthetic batches (the dataset / tokenizer / W&B / Hub plumbing of the
 reference main() is out of scope: SURVEY.md §2a) and writes reference-format checkpoints.
 """
@@ -22,7 +23,6 @@ import time
 import torch
 
 import config
-import data
 import optim
 from model import ImageToTextModel
 
@@ -31,39 +31,66 @@ def _lr_of(optimizer):
     return optimizer.param_groups[0]["lr"]
 
 
+def _fused_loss_ok(model, criterion) -> bool:
+    """The fused step computes nn.CrossEntropyLoss(ignore_index=PAD) with mean reduction
+    (train.py:327); any other criterion runs through autograd on the returned logits."""
+    if criterion is None:
+        return True
+    return (isinstance(criterion, torch.nn.CrossEntropyLoss) and criterion.ignore_index == model.decoder_pad_idx
+            and criterion.reduction == "mean" and criterion.weight is None and criterion.label_smoothing == 0.0)
+
+
+def _staged(model, dataloader):
+    """Batches on the device. Images go to the GPU once, so the next step can consume the encoder
+    output that model.prefetch_encoder computed for this very tensor one step earlier; uint8
+    batches (data.collate_fn) are normalised there by one kernel (model.image_processor)."""
+    for b in dataloader:
+        b = dict(b)
+        if b["images"].dtype == torch.uint8:
+            b["images"] = model.image_processor.normalize(b["images"])
+        else:
+            b["images"] = b["images"].to(model.device, non_blocking=True)
+        yield b
+
+
 def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_value, scheduler, epoch,
                     log_interval, wandb_run, dist=None):
-    """train.py:62-123 on the fused step. Returns the average training loss of the epoch."""
+    """train.py:62-123. Returns the average training loss of the epoch.
+
+    With the fused optimizer (optim.AdamW) and the reference criterion, each batch is ONE kernel
+    sequence (model.train_step: forward + CE + backward, no host sync) plus optimizer.step(clip).
+    With any other optimizer (e.g. torch.optim.AdamW over model.parameters()) or criterion, the
+    reference's own call sequence runs (train.py:80-100): zero_grad, logits = model(...),
+    loss = criterion(...), loss.backward() (the HIP backward via autograd), clip_grad_norm_,
+    optimizer.step()."""
     model.train()
+    fused = isinstance(optimizer, optim.AdamW) and _fused_loss_ok(model, criterion)
+    if dist is not None and not fused:
+        raise ValueError("data-parallel training runs the fused step: pass optim.AdamW and the reference criterion")
     total = torch.zeros(1, dtype=torch.float32, device=model.device)
     n = 0
-
-    pre = None
-
-    def staged(it):
-        # images go to the device once, so the next step can consume the encoder output that
-        # model.prefetch_encoder computed for this very tensor one step earlier; uint8 batches
-        # (data.collate_fn) are normalised there by one kernel (data.to_device)
-        nonlocal pre
-        for b in it:
-            b = dict(b)
-            if b["images"].dtype == torch.uint8:
-                b["images"] = model.image_processor.normalize(b["images"])
-            else:
-                b["images"] = b["images"].to(model.device, non_blocking=True)
-            yield b
-
-    it = staged(dataloader)
+    it = _staged(model, dataloader)
     batch = next(it, None)
     i = -1
     while batch is not None:
         i += 1
         nxt = next(it, None)
-        optimizer.zero_grad()
-        # the frozen encoder of the NEXT batch runs on a second stream during this step
-        loss = model.train_step(batch["images"], batch["decoder_input_tokens"], batch["target_tokens"], dist=dist,
-                                next_images=nxt["images"] if nxt is not None else None)
-        optimizer.step(grad_clip_value if grad_clip_value > 0 else 0.0)
+        if fused:
+            optimizer.zero_grad()
+            # the frozen encoder of the NEXT batch runs on a second stream during this step
+            loss = model.train_step(batch["images"], batch["decoder_input_tokens"], batch["target_tokens"], dist=dist,
+                                    next_images=nxt["images"] if nxt is not None else None)
+            optimizer.step(grad_clip_value if grad_clip_value > 0 else 0.0)
+        else:
+            optimizer.zero_grad()
+            logits = model(batch["images"], batch["decoder_input_tokens"])
+            tgt = batch["target_tokens"].to(model.device)
+            loss = criterion(logits.view(-1, logits.size(-1)), tgt.reshape(-1))
+            loss.backward()
+            if grad_clip_value > 0:
+                torch.nn.utils.clip_grad_norm_(model.parameters(), grad_clip_value)
+            optimizer.step()
+            loss = loss.detach().reshape(1)
         if scheduler:
             scheduler.step()
         total += loss
@@ -80,16 +107,18 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
 
 @torch.no_grad()
 def evaluate(model, dataloader, criterion, device):
-    """train.py:125-151: mean over batches of CE(ignore PAD), no dropout."""
+    """train.py:125-151: mean over batches of the criterion (CE(ignore PAD)), no dropout."""
     model.eval()
     total = torch.zeros(1, dtype=torch.float32, device=model.device)
     n = 0
-    pre = None
-    for batch in dataloader:
-        images = batch["images"]
-        if images.dtype == torch.uint8:  # data.collate_fn batches: normalised on the GPU
-            images = model.image_processor.normalize(images)
-        total += model.eval_loss(images, batch["decoder_input_tokens"], batch["target_tokens"])
+    fused = _fused_loss_ok(model, criterion)
+    for batch in _staged(model, dataloader):
+        if fused:
+            total += model.eval_loss(batch["images"], batch["decoder_input_tokens"], batch["target_tokens"])
+        else:
+            logits = model(batch["images"], batch["decoder_input_tokens"])
+            tgt = batch["target_tokens"].to(model.device)
+            total += criterion(logits.view(-1, logits.size(-1)), tgt.reshape(-1)).reshape(1)
         n += 1
     model.train()
     return (total / max(n, 1)).item()
@@ -152,12 +181,21 @@ def save_checkpoint(model, optimizer, epoch, val_loss, path_prefix, scheduler=No
     return name
 
 
+class CheckpointError(RuntimeError):
+    """A checkpoint that exists but cannot resume this model / optimizer."""
+
+
 def load_checkpoint(model, optimizer, scheduler, path):
-    """train.py:343-375: resume from a .pt checkpoint written by save_checkpoint -> (start_epoch,
-    best_val_loss). A missing or unreadable file means training from scratch (0, inf), as the
-    reference does. Loaded with torch.load(weights_only=True): the dict holds only tensors and
-    plain containers, so nothing in the file is executed (the reference uses weights_only=False).
-    A .safetensors path (inference.py:66-67) restores the model weights only."""
+    """train.py:343-375: resume from a .pt checkpoint (the reference's own or save_checkpoint's) ->
+    (start_epoch, best_val_loss). A missing path means training from scratch (0, inf), as the
+    reference does. A checkpoint that exists but does not fit (unreadable file, missing keys, shape
+    or optimizer-state mismatch) raises CheckpointError BEFORE anything is loaded: the reference
+    falls back to scratch on any error (train.py:362-368), possibly after loading the weights but
+    not the optimizer — a silent half-resume this build refuses.
+    Loaded with torch.load(weights_only=True): tensors and plain containers only, nothing in the
+    file is executed (the reference uses weights_only=False). A .safetensors path
+    (inference.py:66-67) restores the model weights only. The optimizer state may be torch.optim
+    .AdamW's (the reference's, or optim.AdamW's, which writes the same format)."""
     if not path or not os.path.exists(path):
         if path:
             print(f"Warning: checkpoint '{path}' does not exist. Starting training from scratch.")
@@ -165,19 +203,25 @@ def load_checkpoint(model, optimizer, scheduler, path):
     try:
         if path.endswith(".safetensors"):
             from safetensors.torch import load_file
-            model.load_state_dict(load_file(path))
+            sd = load_file(path)
+            model.check_state_dict(sd)
+            model.load_state_dict(sd)
             return 0, math.inf
         ck = torch.load(path, map_location="cpu", weights_only=True)
-        model.load_state_dict(ck["model_state_dict"])
+        for k in ("model_state_dict", "optimizer_state_dict", "epoch"):
+            if k not in ck:
+                raise KeyError(f"checkpoint has no '{k}' (keys: {sorted(ck)})")
+        model.check_state_dict(ck["model_state_dict"])
+        # optim.AdamW.load_state_dict validates everything before it writes (all or nothing)
         optimizer.load_state_dict(ck["optimizer_state_dict"])
-        if scheduler is not None and ck.get("scheduler_state_dict"):
-            scheduler.load_state_dict(ck["scheduler_state_dict"])
-        start = ck["epoch"] + 1
-        print(f"Successfully resumed training. Starting from epoch {start}.")
-        return start, ck.get("best_val_loss", math.inf)
-    except Exception as e:  # noqa: BLE001 — the reference falls back to scratch on any load error
-        print(f"Error loading checkpoint: {e}. Starting training from scratch.")
-        return 0, math.inf
+    except Exception as e:  # noqa: BLE001
+        raise CheckpointError(f"cannot resume from '{path}': {e}") from e
+    model.load_state_dict(ck["model_state_dict"])
+    if scheduler is not None and ck.get("scheduler_state_dict"):
+        scheduler.load_state_dict(ck["scheduler_state_dict"])
+    start = ck["epoch"] + 1
+    print(f"Successfully resumed training. Starting from epoch {start}.")
+    return start, ck.get("best_val_loss", math.inf)
 
 
 def main(argv=None):
@@ -193,7 +237,7 @@ def main(argv=None):
     torch.manual_seed(config.RANDOM_SEED)
     model = ImageToTextModel(config.VOCAB_SIZE, config.DECODER_EMBED_DIM, config.DECODER_HEADS, config.DECODER_LAYERS,
                              config.DECODER_FF_DIM, config.MAX_SEQ_LEN, config.DECODER_DROPOUT, config.PAD_TOKEN_ID)
-    opt = optim.AdamW(model.store, lr=config.LEARNING_RATE, betas=(config.ADAM_BETA1, config.ADAM_BETA2),
+    opt = optim.AdamW(model.parameters(), lr=config.LEARNING_RATE, betas=(config.ADAM_BETA1, config.ADAM_BETA2),
                       eps=config.ADAM_EPS, weight_decay=config.WEIGHT_DECAY)
     sched = None
     if config.WARMUP_STEPS > 0:

@@ -100,3 +100,62 @@ def test_inference_postprocess_matches_reference_rules():
     assert postprocess_ids([], S, E) == []
     assert clean_text("  a <UNK> dog   on<UNK> grass ") == "a dog on grass"
     assert clean_text("<UNK>") == ""
+
+
+def _cpu_store(meta, n_enc):
+    from decoder import decoder_entries
+    from params import FlatParams
+    dec = FX.dec_desc(meta)
+    E = FX.enc_desc(meta)["hidden"]
+    proj = E if E != dec["d"] else None
+    store = FlatParams(decoder_entries(dec["vocab"], dec["d"], dec["layers"], dec["ff"], proj), torch.device("cpu"),
+                       torch.float32)
+    store.vocab = dec["vocab"]
+    store.layout = dict(V=dec["vocab"], d=dec["d"], L=dec["layers"], F=dec["ff"], proj_in=proj, n_encoder_params=n_enc)
+    return store
+
+
+@pytest.mark.parametrize("name", ["tiny_vit_patches", "tiny_vit_v509", "tiny_clip336_cls"])
+def test_optimizer_state_maps_torch_adamw_format(name):
+    """optim.AdamW speaks torch.optim.AdamW's state_dict in the reference's parameter order
+    (train.py:319-325 builds the optimizer over model.parameters(): frozen encoder first): a state
+    produced by torch over the reference-shaped parameters loads into the flat moments, and
+    state_dict() gives it back; a mismatching state is rejected with nothing written."""
+    import optim
+    meta, _ = FX.load(name)
+    spec = [(n, tuple(s)) for n, s in meta["spec"]]
+    n_enc = sum(1 for n, _ in spec if n.startswith("encoder."))
+    store = _cpu_store(meta, n_enc)
+    assert [n for n, _ in optim.reference_trainable(store.layout)] == [n for n, _ in spec if not n.startswith("encoder.")]
+    params = [torch.nn.Parameter(torch.randn(s)) for _, s in spec]
+    topt = torch.optim.AdamW(params, lr=3e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-5)
+    for i, (n, _) in enumerate(spec):
+        if not n.startswith("encoder."):
+            params[i].grad = torch.randn_like(params[i])
+    topt.step()
+    topt.step()
+    sd = topt.state_dict()
+    opt = optim.AdamW(store, lr=1.0)
+    opt.load_state_dict(sd)
+    assert opt.param_groups[0]["lr"] == 3e-4 and int(opt.step_t.item()) == 2
+    back = opt.state_dict()
+    assert back["param_groups"][0]["params"] == sd["param_groups"][0]["params"]
+    assert set(back["state"]) == set(sd["state"])
+    for i, s in sd["state"].items():
+        for k in ("exp_avg", "exp_avg_sq"):
+            torch.testing.assert_close(back["state"][i][k], s[k], rtol=0, atol=0)
+        assert float(back["state"][i]["step"]) == float(s["step"])
+    # padded head: the pad rows of the moments stay zero
+    V = store.vocab
+    fo = optim._BufView(store, store.exp_avg).p("fc_out.weight")
+    assert torch.count_nonzero(fo[V:]) == 0
+    # mismatches raise and leave the state alone
+    before = store.exp_avg.clone()
+    bad = {"state": dict(sd["state"]), "param_groups": sd["param_groups"]}
+    k0 = max(bad["state"])
+    bad["state"][k0] = dict(bad["state"][k0], exp_avg=torch.zeros(3))
+    with pytest.raises(optim.OptimizerStateError):
+        opt.load_state_dict(bad)
+    with pytest.raises(optim.OptimizerStateError):
+        opt.load_state_dict({"step": 1, "exp_avg": before})
+    assert torch.equal(store.exp_avg, before)

@@ -258,6 +258,28 @@ def test_embed_ce_colsum(dtype):
     tr = table.clone().requires_grad_(True)
     (F.embedding(tok, tr, padding_idx=0) * math.sqrt(d)).backward(dx.float())
     _close(dtab, tr.grad, 1e-5)
+    # deterministic (planned) path: same values, bit-identical on every repeat, also with repeated
+    # tokens (a frequent word), dropout and d = 768
+    for dd, p in ((d, 0.0), (768, 0.1)):
+        tk = tok.clone()
+        tk[0, ::3] = 7
+        tk[2, 5:15] = 7
+        dxx = torch.randn(B, T, dd, device=dev()).to(dtype)
+        plan = torch.empty(N.embed_plan_ints(tk.numel()), dtype=torch.int32, device=dev())
+        N.embed_plan(tk, plan)
+        seed = torch.tensor([5], dtype=torch.int64, device=dev())
+        outs = []
+        for _ in range(3):
+            dt = torch.zeros(V, dd, device=dev())
+            N.embed_bwd(tk, dxx, 2.0, dt, 0, drop_p=p, seed=seed, site=4000, plan=plan)
+            outs.append(dt)
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+        mk = torch.ones(B * T * dd, device=dev())
+        if p > 0:
+            N.dropout_mask(mk.numel(), p, seed, 4000, mk)
+        tr = torch.zeros(V, dd, device=dev(), requires_grad=True)
+        (F.embedding(tk, tr, padding_idx=0) * 2.0).backward(dxx.float() * mk.view(B, T, dd))
+        _close(outs[0], tr.grad, 1e-5)
     # cross entropy with ignore
     rows = 300
     logits = torch.randn(rows, V, device=dev()).to(dtype)

@@ -270,13 +270,10 @@ def test_encoder_prefetch_matches_inline():
             opt.step(5.0)
         res.append((losses, m.store.master.clone()))
     (l0, p0), (l1, p1) = res
-    assert all(abs(a - b) < 1e-5 for a, b in zip(l0, l1)), (l0, l1)
-    # the embedding gradient is a float atomic scatter-add (summation order varies run to run);
-    # AdamW's g/sqrt(v) turns last-ulp differences of near-zero gradients into update-sized ones
-    # (<= 2 lr) on a few elements — the same spread two inline runs show
-    diff = (p1 - p0).abs()
-    assert diff.max().item() <= 2.5e-3
-    assert (diff > 1e-5).float().mean().item() < 5e-3
+    # every reduction of the step sums in a fixed order (split-K slabs, LayerNorm partials, CE rows,
+    # the planned embedding scatter): the two schedules are bit-identical
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(p1, p0)
 
 
 def test_checkpoint_save_resume_roundtrip(tmp_path):
@@ -311,9 +308,9 @@ def test_checkpoint_save_resume_roundtrip(tmp_path):
     m2, opt2, sch2 = fresh()
     start, best = TR.load_checkpoint(m2, opt2, sch2, name + ".pt")
     assert start == 1 and abs(best - 1.2345) < 1e-9
-    # up to float-atomic summation order (the embedding-gradient scatter-add)
-    assert abs(step(m2, opt2, sch2, batches[2]) - ref_next) <= 1e-5 * abs(ref_next)
-    torch.testing.assert_close(m2.store.master, ref_params, rtol=1e-5, atol=1e-6)
+    # deterministic step: the resumed run continues bit-identically
+    assert step(m2, opt2, sch2, batches[2]) == ref_next
+    assert torch.equal(m2.store.master, ref_params)
 
     m3, opt3, sch3 = fresh()
     assert TR.load_checkpoint(m3, opt3, sch3, name + ".safetensors") == (0, float("inf"))
