@@ -206,26 +206,54 @@ def synthetic_batch(B, seq_len, vocab, device, seed, image=224):
     return images, cap[:, :-1].contiguous().to(device), cap[:, 1:].contiguous().to(device)
 
 
+def _cpu_threads() -> int:
+    """The threads this job may use on the host: OMP_NUM_THREADS (the GPU box sets it to the job's CPU
+    share, 16 per GPU; os.cpu_count() there reports the whole machine), else every CPU."""
+    try:
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(model, args):
-    """The CPU oracle's train step (fp32, torch CPU, dropout off) on a bounded sample of the same
-    workload: cfg1 architecture, patches mode, `cpu_batch` pairs per step, same weights."""
+    """The CPU oracle's train step (oracle/ref_cpu.py: fp32 torch CPU restatement of the reference
+    path, pinned to the reference's outputs; dropout off) on bounded samples (SURVEY.md §8d / BASELINE.md
+    §3): configs[1]'s architecture in patches mode (the metric's workload -> `value`) and cls mode,
+    and configs[0] (2L d128 H8 decoder + ViT-B/16, batch 4, seq_len 32, cls = the reference's own
+    path). Same ViT-B/16 weights as the GPU model; median of `cpu_steps` steps after a warm-up."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle import ref_cpu as R
+    import optim
+    threads = _cpu_threads()
+    torch.set_num_threads(threads)
     sd = {k: v.float().cpu() for k, v in model.state_dict().items()}
-    names = [k for k in sd if not k.startswith("encoder.") and not k.endswith("positional_encoding.pe")]
     enc = {"kind": "vit", "heads": 12, "layers": 12, "patch": 16, "eps": 1e-12}
-    dec = {"heads": 8, "layers": 6, "max_seq_len": 100}
+
+    def timed(params, names, dec, mode, B, seq_len):
+        images, di, tg = synthetic_batch(B, seq_len, args.vocab, "cpu", 7)
+        opt = R.AdamWState({k: params[k] for k in names})
+        R.train_step(params, names, opt, images, di, tg, enc, dec, mode, 5.0)  # warm-up
+        times = []
+        for _ in range(args.cpu_steps):
+            t0 = time.perf_counter()
+            R.train_step(params, names, opt, images, di, tg, enc, dec, mode, 5.0)
+            times.append(time.perf_counter() - t0)
+        return B / sorted(times)[len(times) // 2]
+
+    names1 = [k for k in sd if not k.startswith("encoder.") and not k.endswith("positional_encoding.pe")]
+    dec1 = {"heads": 8, "layers": 6, "max_seq_len": 100}
     B = args.cpu_batch
-    images, di, tg = synthetic_batch(B, args.seq_len, args.vocab, "cpu", 7)
-    opt = R.AdamWState({k: sd[k] for k in names})
-    R.train_step(sd, names, opt, images, di, tg, enc, dec, args.memory_mode, 5.0)  # warm-up
-    times = []
-    for _ in range(args.cpu_steps):
-        t0 = time.perf_counter()
-        R.train_step(sd, names, opt, images, di, tg, enc, dec, args.memory_mode, 5.0)
-        times.append(time.perf_counter() - t0)
-    times.sort()
-    med = times[len(times) // 2]
+    v_patches = timed(dict(sd), names1, dec1, "patches", B, args.seq_len)
+    v_cls = timed(dict(sd), names1, dec1, "cls", B, args.seq_len)
+    # configs[0]: the same encoder + a seeded 2L d128 / 8-head decoder in the reference's tensor names
+    lay0 = dict(V=args.vocab, d=128, L=2, F=512, proj_in=768)
+    g = torch.Generator().manual_seed(0)
+    p0 = {k: v for k, v in sd.items() if k.startswith("encoder.")}
+    for n, shp in optim.reference_trainable(lay0):
+        t = torch.randn(*shp, generator=g)
+        p0[n] = t / (shp[1] ** 0.5) if len(shp) == 2 else 0.02 * t
+    names0 = [n for n, _ in optim.reference_trainable(lay0)]
+    v_cfg0 = timed(p0, names0, {"heads": 8, "layers": 2, "max_seq_len": 100}, "cls", 4, 32)
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -235,9 +263,13 @@ def cpu_baseline(model, args):
                     break
     except OSError:
         pass
-    return {"value": B / med, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/ref_cpu.py fp32 train step, cfg1 architecture ({args.memory_mode}), batch {B}, "
-                      f"median of {args.cpu_steps} steps after 1 warm-up, dropout off; cpu: {cpu_model}"}
+    return {"value": round(v_patches, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ref_cpu.py fp32 train step (encoder fwd + decoder fwd/bwd + clip + AdamW), configs[1] "
+                      f"architecture, patches mode, batch {B}, seq_len {args.seq_len}; median of {args.cpu_steps} steps "
+                      f"after 1 warm-up, dropout off; {threads} threads = this job's CPU share (OMP_NUM_THREADS); "
+                      f"cpu: {cpu_model}",
+            "also": {"configs[1] cls mode (the reference's CLS-only memory)": round(v_cls, 3),
+                     "configs[0] (2L d128 H8 + ViT-B/16, batch 4, seq_len 32, cls)": round(v_cfg0, 3)}}
 
 
 def bench_decode(args):

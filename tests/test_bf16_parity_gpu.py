@@ -1,0 +1,51 @@
+"""bf16 parity of the benchmarked (MFMA) path, per golden fixture, against the reference's fp32
+outputs AND calibrated against the reference's own bf16 error: the same reference code run under
+torch.autocast(bfloat16) (tests/golden/make_bf16_calibration.py -> bf16_reference_calibration.json).
+
+The north star's "logits within 1e-2 bf16" is read as RELATIVE (relative L2 over the pinned logits):
+the reference itself, in bf16, is 2.5e-2 .. 4.3e-2 off in max-abs on these fixtures (logit scale ~4),
+so no bf16 implementation meets 1e-2 absolute; DESIGN.md §6 has the table. Bounds:
+  logits   rel-L2 <= 1e-2 and <= 1.5x the reference-bf16 rel-L2; max-abs <= 1.5x the reference-bf16
+           max-abs; argmax identical wherever the reference's top-1/top-2 margin > 5e-2
+  encoder  rel-L2 <= 2x the reference-bf16 encoder error (our residual stream is bf16, autocast's f32)
+  step     loss within 5e-3, pre-clip grad norm within 1 %; per-tensor gradient error RMS / tensor RMS:
+           median <= 1.6x reference-bf16 + 0.01, worst tensor <= 2.5x reference-bf16's worst; every
+           tensor's norm within 10 %."""
+import json
+import os
+
+import pytest
+import torch
+
+import fixtures as FX
+
+pytestmark = pytest.mark.gpu
+
+CAL = json.load(open(os.path.join(FX.GOLDEN, "bf16_reference_calibration.json")))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("name", FX.CASES)
+def test_bf16_within_reference_bf16_envelope(name):
+    from parity_metrics import case_metrics
+    r = case_metrics(name, torch.bfloat16)
+    c = CAL[name]
+    print(f"{name}: logits rel {r['logits_rel_l2']:.2e} (ref-bf16 {c['logits_rel_l2']:.2e}) max-abs "
+          f"{r['logits_max_abs']:.3f} ({c['logits_max_abs']:.3f}); enc {r['enc_rel_l2']:.2e} ({c['enc_rel_l2']:.2e}); "
+          f"grad rms median {r['grad_rms_median']:.3f} ({c['grad_rms_median']:.3f}) max {r['grad_rms_max']:.3f} "
+          f"({c['grad_rms_max']:.3f})")
+    assert r["logits_rel_l2"] <= 1e-2
+    assert r["logits_rel_l2"] <= 1.5 * c["logits_rel_l2"]
+    assert r["logits_max_abs"] <= 1.5 * c["logits_max_abs"]
+    assert r["argmax_agree_margin_gt_5e-2"] == 1.0
+    assert r["enc_rel_l2"] <= 2.0 * c["enc_rel_l2"]
+    assert r["step1_loss_abs_err"] <= 5e-3
+    assert r["grad_norm_rel_err"] <= 1e-2
+    assert r["grad_rms_median"] <= 1.6 * c["grad_rms_median"] + 0.01
+    assert r["grad_rms_max"] <= 2.5 * c["grad_rms_max"]
+    assert r["grad_norm_rel_err_max"] <= 0.1
