@@ -376,10 +376,12 @@ class TransformerDecoder:
 
     def run_forward(self, tokens: torch.Tensor, mem: torch.Tensor, mem_ld: int, S: int, A: _Acts,
                     seed: Optional[torch.Tensor], train: bool, logits_out: Optional[torch.Tensor] = None,
-                    drop_p: Optional[float] = None):
+                    drop_p: Optional[float] = None, mem_keys: Optional[torch.Tensor] = None):
         """tokens int64 [B,T] (device); mem: memory rows [B*S, d] with row stride mem_ld.
         train=True keeps every layer's activations for run_backward (A must be a train arena);
-        drop_p defaults to the module's dropout in train mode and 0 otherwise."""
+        drop_p defaults to the module's dropout in train mode and 0 otherwise.
+        mem_keys: optional int64 [B, S], 0 where the memory key is padding (memory_padding_mask,
+        decoder.py:134-186 -> memory_key_padding_mask of nn.TransformerDecoder), else 1."""
         B, T = tokens.shape
         d, H, L, V = self.d, self.H, self.L, self.V
         st = self.store
@@ -412,7 +414,7 @@ class TransformerDecoder:
             kvl = A.kv[:, l * 2 * d:]
             ca = native.attn_args(A.qc[j], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
                                   S * L * 2 * d, A.oc[j], d, T * d, lse=A.lse_c[j], scale=1.0 / math.sqrt(self.hd), drop_p=p,
-                                  seed=seed, site=base + 2)
+                                  seed=seed, site=base + 2, key_tokens=mem_keys, tok_batch=S, pad_idx=0)
             native.attention_fwd(native.dtype_code(qkv), B, H, T, S, ca, Dh=self.hd)
             native.linear(A.oc[j], w(pre + "cross_out.weight"), A.y, bias=st.p(pre + "cross_out.bias"), workspace=ws)
             native.layernorm_fwd(xs[0], st.p(pre + "norm2.weight"), st.p(pre + "norm2.bias"), 1e-5, xs[1], r=A.y,
@@ -430,7 +432,8 @@ class TransformerDecoder:
     def run_backward(self, tokens: torch.Tensor, mem: torch.Tensor, mem_ld: int, S: int, A: _Acts,
                      seed: Optional[torch.Tensor], dlogits: torch.Tensor,
                      proj_input: Optional[Tuple[torch.Tensor, int, int]] = None,
-                     grads_ready: Optional[Callable[[str, str], None]] = None):
+                     grads_ready: Optional[Callable[[str, str], None]] = None,
+                     mem_keys: Optional[torch.Tensor] = None):
         """Backward of run_forward(train=True) given dlogits [R, V] (compute dtype).
         proj_input = (enc_rows, ld, E): encoder features feeding the projection (for dW_proj).
         grads_ready(first, last) is called as soon as the grads of a contiguous entry span are final."""
@@ -516,7 +519,7 @@ class TransformerDecoder:
             kvl, dkvl = A.kv[:, l * 2 * d:], A.dkv[:, l * 2 * d:]
             ca = native.attn_args(A.qc[l], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d,
                                   S * L * 2 * d, A.oc[l], d, T * d, lse=A.lse_c[l], scale=1.0 / math.sqrt(self.hd), drop_p=p,
-                                  seed=seed, site=base + 2)
+                                  seed=seed, site=base + 2, key_tokens=mem_keys, tok_batch=S, pad_idx=0)
             cg = native.attn_grads(A.do, d, T * d, A.dq, d, T * d, dkvl, L * 2 * d, S * L * 2 * d, dkvl[:, d:],
                                    L * 2 * d, S * L * 2 * d, A.delta)
             guard(A.dq)
@@ -611,16 +614,22 @@ class TransformerDecoder:
 
     def forward(self, tgt_tokens: torch.Tensor, memory: torch.Tensor, memory_padding_mask=None) -> torch.Tensor:
         """decoder.py:134-193: f32 logits [B, T, V] (no autograd; training goes through the model's
-        fused train step)."""
-        if memory_padding_mask is not None:
-            raise NotImplementedError("memory_padding_mask: the reference never passes one (model.py:158)")
+        train step). memory_padding_mask: bool [B, S], True = padded memory position, masked out of
+        the cross-attention (memory_key_padding_mask, decoder.py:179-186); a query whose memory is
+        all padding gets NaN, like the reference."""
         tokens = tgt_tokens.to(self.device, torch.int64).contiguous()
         B, T = tokens.shape
         S = memory.shape[1]
+        self.store.ensure_shadow()
         mem = memory.to(self.device, self.dtype).reshape(B * S, self.d).contiguous()
+        keys = None
+        if memory_padding_mask is not None:
+            if tuple(memory_padding_mask.shape) != (B, S):
+                raise ValueError(f"memory_padding_mask must be [B, S] = {(B, S)}, got {tuple(memory_padding_mask.shape)}")
+            keys = (~memory_padding_mask.to(self.device, torch.bool)).to(torch.int64).contiguous()
         A = self.acts(B, T, S, False)
         out = torch.empty(B * T, self.Vp, dtype=torch.float32, device=self.device)
-        self.run_forward(tokens, mem, self.d, S, A, None, False, logits_out=out)
+        self.run_forward(tokens, mem, self.d, S, A, None, False, logits_out=out, mem_keys=keys)
         return self.unpad_logits(out, B, T)
 
     __call__ = forward

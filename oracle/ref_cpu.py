@@ -126,13 +126,16 @@ def _mha(q_in, kv_in, w_in, b_in, w_out, b_out, heads, mask=None, drop=None):
 
 def decoder_forward(p: Params, tokens: torch.Tensor, memory: torch.Tensor, *, heads: int, layers: int,
                     pad_idx: int = 0, max_len: int = 100, prefix: str = "decoder.",
-                    drops: Optional[dict] = None, return_hidden: bool = False):
+                    drops: Optional[dict] = None, return_hidden: bool = False,
+                    memory_padding_mask: Optional[torch.Tensor] = None):
     """decoder.TransformerDecoder.forward (decoder.py:134-193):
     causal mask (utils.py:30-36) + key-padding mask tok==PAD (utils.py:66), Emb*sqrt(d) + PE
     (decoder.py:168-171), L x nn.TransformerDecoderLayer post-LN / ReLU / eps 1e-5
     (torch/nn/modules/transformer.py:1131-1199), fc_out (decoder.py:191).
     ``drops`` (test hook): {site: multiplier tensor} pre-scaled dropout masks, keys
-    'emb', f'{i}.sa', f'{i}.d1', f'{i}.ca', f'{i}.d2', f'{i}.ff', f'{i}.d3'."""
+    'emb', f'{i}.sa', f'{i}.d1', f'{i}.ca', f'{i}.d2', f'{i}.ff', f'{i}.d3'.
+    ``memory_padding_mask`` bool [B, S] (True = pad): memory_key_padding_mask of the cross-attention
+    (decoder.py:179-186), a -inf additive mask on those keys."""
     g = lambda k: p[prefix + k]  # noqa: E731
     dr = drops or {}
     b, t = tokens.shape
@@ -140,6 +143,9 @@ def decoder_forward(p: Params, tokens: torch.Tensor, memory: torch.Tensor, *, he
     causal = torch.triu(torch.full((t, t), float("-inf")), diagonal=1)
     kpm = torch.zeros(b, 1, 1, t).masked_fill((tokens == pad_idx).view(b, 1, 1, t), float("-inf"))
     mask = causal.view(1, 1, t, t) + kpm
+    mmask = None
+    if memory_padding_mask is not None:
+        mmask = torch.zeros(b, 1, 1, memory.shape[1]).masked_fill(memory_padding_mask.view(b, 1, 1, -1), float("-inf"))
     x = F.embedding(tokens, g("token_embedding.weight")) * math.sqrt(d)
     x = x + sinusoidal_pe(max_len, d)[:t].unsqueeze(0)
     if "emb" in dr:
@@ -154,7 +160,7 @@ def decoder_forward(p: Params, tokens: torch.Tensor, memory: torch.Tensor, *, he
         x = F.layer_norm(x + sa, (d,), g(L + "norm1.weight"), g(L + "norm1.bias"), 1e-5)
         ca = _mha(x, memory, g(L + "multihead_attn.in_proj_weight"), g(L + "multihead_attn.in_proj_bias"),
                   g(L + "multihead_attn.out_proj.weight"), g(L + "multihead_attn.out_proj.bias"), heads,
-                  None, dr.get(f"{i}.ca"))
+                  mmask, dr.get(f"{i}.ca"))
         if f"{i}.d2" in dr:
             ca = ca * dr[f"{i}.d2"]
         x = F.layer_norm(x + ca, (d,), g(L + "norm2.weight"), g(L + "norm2.bias"), 1e-5)

@@ -307,6 +307,35 @@ def run_gen_case(name, enc_kind, enc_cfg, dec, *, n_images, seed, image_size, ma
     print(f"{name}: {[len(r) for r in ids]} ids, min margin {min(min(x) for x in margins):.4f}", flush=True)
 
 
+def run_memory_mask_case(name, dec, *, B, T, S, mem_lengths, seed):
+    """The reference decoder alone (decoder.TransformerDecoder.forward, decoder.py:134-193) with a
+    memory_padding_mask (True = padded memory position), which model.forward never passes."""
+    torch.manual_seed(0)
+    m = ref_decoder.TransformerDecoder(vocab_size=dec["vocab"], embed_dim=dec["embed_dim"], num_heads=dec["heads"],
+                                       num_layers=dec["layers"], ff_dim=dec["ff"], max_seq_len=100, dropout=0.0,
+                                       pad_idx=0)
+    spec = [("decoder." + n, tuple(p.shape)) for n, p in m.named_parameters()]
+    state = P.make_state(spec, seed)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            p.copy_(state["decoder." + n])
+    m.eval()
+    g = torch.Generator().manual_seed(seed + 1)
+    memory = torch.randn(B, S, dec["embed_dim"], generator=g)
+    mask = torch.zeros(B, S, dtype=torch.bool)
+    for i, n in enumerate(mem_lengths):
+        mask[i, n:] = True
+    tokens = P.make_captions(B, T, dec["vocab"], seed + 2, [T, T - 5, 3][:B])
+    with torch.no_grad():
+        logits = m(tokens, memory, memory_padding_mask=mask)
+    meta = {"case": name, "dec": dec, "B": B, "T": T, "S": S, "mem_lengths": mem_lengths, "seed": seed,
+            "spec": [[n, list(s)] for n, s in spec], "weights_checksum": P.checksum(state[n] for n, _ in spec)}
+    path = os.path.join(HERE, f"{name}.safetensors")
+    save_file({"logits": logits.contiguous(), "memory": memory.contiguous(), "tokens": tokens.float()}, path,
+              metadata={"meta": json.dumps(meta)})
+    print(f"{name}: {os.path.getsize(path) / 1e6:.2f} MB", flush=True)
+
+
 TINY_VIT = dict(hidden_size=128, num_hidden_layers=2, num_attention_heads=2, intermediate_size=512,
                 image_size=224, patch_size=16)
 TINY_CLIP = dict(hidden_size=128, num_hidden_layers=2, num_attention_heads=2, intermediate_size=512,
@@ -369,6 +398,8 @@ if __name__ == "__main__":
         # configs[4] parity anchor: the cfg1 architecture with the cfg1_b2_patches weights (seed 21)
         run_gen_case("cfg1_gen_cls", "vit", {}, CFG1_DEC, n_images=4, seed=21, image_size=224, max_len=16,
                      start=ref_config.START_TOKEN_ID, end=ref_config.END_TOKEN_ID)
+    if want("dec_memory_mask"):
+        run_memory_mask_case("dec_memory_mask", TINY_DEC96, B=3, T=17, S=37, mem_lengths=[37, 20, 5], seed=81)
     if want("dp2_tiny"):
         run_dp_case("dp2_tiny", "vit", TINY_VIT, TINY_DEC96, B=8, cap_len=20,
                     lengths=[20, 20, 18, 20, 7, 9, 11, 5], seed=31, image_size=224)

@@ -322,3 +322,31 @@ def test_checkpoint_save_resume_roundtrip(tmp_path):
     with torch.no_grad():
         torch.testing.assert_close(m3(imgs, di), m2b(imgs, di), rtol=0, atol=0)
     assert TR.load_checkpoint(m3, opt3, sch3, str(tmp_path / "missing.pt")) == (0, float("inf"))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_decoder_memory_padding_mask_matches_reference(dtype):
+    """TransformerDecoder.forward(tokens, memory, memory_padding_mask) against the reference decoder
+    (fixture dec_memory_mask: memory rows past each length are padding)."""
+    from decoder import TransformerDecoder, reference_to_flat
+    meta, T = FX.load("dec_memory_mask")
+    st = FX.state(meta)
+    d = meta["dec"]
+    dec = TransformerDecoder(d["vocab"], d["embed_dim"], d["heads"], d["layers"], d["ff"], 100, 0.0, 0, dtype=dtype)
+    flat = reference_to_flat(st, d["layers"], d["embed_dim"])
+    for k, v in flat.items():
+        dec.store.p(k).copy_(v.cuda())
+    dec.store.sync_shadow()
+    dec.eval()
+    B, S = meta["B"], meta["S"]
+    mask = torch.zeros(B, S, dtype=torch.bool)
+    for i, n in enumerate(meta["mem_lengths"]):
+        mask[i, n:] = True
+    logits = dec(T["tokens"].long().cuda(), T["memory"].cuda(), memory_padding_mask=mask).cpu()
+    ref = T["logits"]
+    if dtype == torch.float32:
+        torch.testing.assert_close(logits, ref, rtol=0, atol=1e-3)
+    else:
+        assert ((logits - ref).norm() / ref.norm()).item() <= 1e-2
+    # the mask matters: without it the logits differ
+    assert (dec(T["tokens"].long().cuda(), T["memory"].cuda()).cpu() - ref).abs().max().item() > 1e-2

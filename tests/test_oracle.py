@@ -101,3 +101,18 @@ def test_procedural_inputs_stable():
     import procedural as P
     imgs, di, tg = FX.inputs(meta, 0)
     assert abs(P.checksum([imgs]) - meta["images_checksum"]) < 1e-6 * abs(meta["images_checksum"]) + 1e-6
+
+
+def test_oracle_decoder_memory_padding_mask():
+    """decoder.TransformerDecoder.forward(tokens, memory, memory_padding_mask) (decoder.py:134-193)."""
+    meta, T = FX.load("dec_memory_mask")
+    st = FX.state(meta)
+    B, S = meta["B"], meta["S"]
+    mask = torch.zeros(B, S, dtype=torch.bool)
+    for i, n in enumerate(meta["mem_lengths"]):
+        mask[i, n:] = True
+    d = meta["dec"]
+    with torch.no_grad():
+        logits = R.decoder_forward(st, T["tokens"].long(), T["memory"], heads=d["heads"], layers=d["layers"],
+                                   memory_padding_mask=mask)
+    torch.testing.assert_close(logits, T["logits"], rtol=1e-4, atol=1e-4)
