@@ -325,6 +325,9 @@ def main():
                          "weight-gradient stream run beside the main stream (measured faster than the graph, whose "
                          "parallel branches ROCm 7 does not overlap)")
     ap.add_argument("--no-graph", action="store_true", help="(default; kept for older scripts)")
+    ap.add_argument("--no-replay", action="store_true",
+                    help="issue every step from Python (eager launches). Default: the step's launches are recorded "
+                         "once (native.record, mit_plan_*) and replayed from C++ per step, same streams and order")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="run the frozen encoder inside each step instead of one step ahead on a second stream")
     ap.add_argument("--workload", default="train", choices=["train", "clip336", "cfg3", "decode"],
@@ -356,6 +359,7 @@ def main():
         return model.train_step(images, di, tg, dist=dp, next_images=images if prefetch else None)
 
     use_graph = world == 1 and args.graph and not args.no_graph
+    replay = not args.no_replay and not use_graph
     if use_graph:
         gstep = model.make_graphed_step(opt, images, di, tg, 5.0)
 
@@ -374,6 +378,21 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if replay:
+        # two consecutive real steps recorded (the encoder prefetch alternates between two arenas),
+        # then replayed alternately: one C++ call per native segment instead of a Python wrapper per launch
+        import native
+        progs = [native.record(step) for _ in range(2)]
+        n_launch = progs[0].launches()
+        out_loss = model.decoder.acts(args.batch, args.seq_len - 1, 1 if args.memory_mode == "cls" else model.encoder.N,
+                                      True).loss
+        it = [0]
+
+        def step():
+            opt._sync_lr()
+            progs[it[0] % 2].run()
+            it[0] += 1
+            return out_loss
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -405,6 +424,8 @@ def main():
         "step_mfma_frac": round(value / world * flops_pair / (MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
         # ~ms_per_step when the host's launch path, not the GPU, paces the step
         "host_enqueue_ms_per_step": round(1e3 * t_enq / args.steps, 3),
+        "launch_path": ("native replay (mit_plan_run), %d launches/step" % n_launch) if replay else
+                       ("hipGraph" if use_graph else "eager (Python per launch)"),
         "final_loss": round(loss, 4),
     }
     if not args.no_roofline:

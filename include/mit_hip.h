@@ -37,6 +37,24 @@ const char* mit_last_error(void);
 int mit_abi_version(void);
 
 /* ---------------------------------------------------------------------------------------------
+ * Launch plans (the host runtime of a train step; no reference counterpart — the reference's
+ * per-op Python dispatch, train.py:80-100, is what it removes from the critical path).
+ * mit_plan_begin() starts recording on the calling thread: every launching entry point below (and
+ * mit_event_record / mit_stream_wait_event) still runs normally and ALSO appends a replay closure
+ * with its arguments copied by value. mit_plan_end() stops and returns the plan; mit_plan_run()
+ * re-issues the recorded launches, in order, on the recorded streams (device pointers and scalars
+ * are fixed; per-step values must live in device memory, as they do in the train step). Host work
+ * between launches (a collective) is not recorded: end the plan there and begin another. */
+void* mit_plan_begin(void);
+void* mit_plan_end(void);
+long mit_plan_size(const void* plan);
+int mit_plan_run(const void* plan);
+void mit_plan_destroy(void* plan);
+/* hipEventRecord / hipStreamWaitEvent on hipEvent_t / hipStream_t handles passed as void* (recordable) */
+int mit_event_record(void* event, void* stream);
+int mit_stream_wait_event(void* stream, void* event);
+
+/* ---------------------------------------------------------------------------------------------
  * GEMM with fused epilogue. Replaces every nn.Linear / F.linear / addmm / mm of the hot path:
  *   encoder  tf/models/vit/modeling_vit.py:213-215,233,249-254 (q/k/v, o_proj, fc1+GELU, fc2+res)
  *            tf/models/clip/modeling_clip.py:338-350 (fc1 + quick_gelu)
@@ -189,9 +207,10 @@ int mit_embed_fwd(int dtype, long B, long T, long d, const int64_t* tokens, cons
                   const float* pe, float drop_p, const uint64_t* seed, uint32_t site, void* out, void* stream);
 /* dtable[tok] += scale * dropout_mask * dx (f32; caller zeroes dtable); the padding_idx row receives
  * no gradient (nn.Embedding(padding_idx=PAD), decoder.py:105; embedding backward of autograd).
- * plan != NULL: DETERMINISTIC — each token's row is the sum of its positions' rows in a fixed order
- * (d <= 1024); plan = int32 [mit_embed_plan_ints(B*T)] filled by mit_embed_plan from the same tokens
- * (any time after the tokens are final). plan == NULL: float atomics (order-dependent rounding). */
+ * plan != NULL: DETERMINISTIC — each token's row is the sum of its positions' rows in position order
+ * (d % 8 == 0, B*T <= 16384); plan = int32 [mit_embed_plan_ints(B*T)] filled by mit_embed_plan from
+ * the same tokens (one workgroup sorts (token, position); any time after the tokens are final).
+ * plan == NULL: float atomics (order-dependent rounding). */
 long mit_embed_plan_ints(long n);
 int mit_embed_plan(const int64_t* tokens, long n, int* plan, void* stream);
 int mit_embed_bwd(int dtype, long B, long T, long d, const int64_t* tokens, const void* dx, float scale, float drop_p,

@@ -1053,6 +1053,7 @@ AttnK make_k(const mit_attn_args* x) {
 extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, long Dh, const mit_attn_args* x,
                                  void* stream) {
   MIT_CHECK_ARG(x && x->q && x->k && x->v && x->o, "mit_attention_fwd: null pointer");
+  MIT_RECORD([=, c = *x]() { return mit_attention_fwd(dtype, B, H, Lq, Lk, Dh, &c, stream); });
   MIT_CHECK_ARG(head_dim_ok(Dh), "mit_attention_fwd: head_dim %ld unsupported (16, 32, 64, 128)", Dh);
   if (B <= 0 || H <= 0 || Lq <= 0) return MIT_OK;
   MIT_CHECK_ARG(Lk > 0, "mit_attention_fwd: Lk must be > 0");
@@ -1108,6 +1109,7 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
                                  const mit_attn_grads* gg, void* stream) {
   MIT_CHECK_ARG(x && gg && x->q && x->k && x->v && x->o && x->lse, "mit_attention_bwd: null forward pointer");
   MIT_CHECK_ARG(gg->dout && gg->dq && gg->dk && gg->dv && gg->delta_ws, "mit_attention_bwd: null grad pointer");
+  MIT_RECORD([=, c = *x, cg = *gg]() { return mit_attention_bwd(dtype, B, H, Lq, Lk, Dh, &c, &cg, stream); });
   MIT_CHECK_ARG(head_dim_ok(Dh), "mit_attention_bwd: head_dim %ld unsupported (16, 32, 64, 128)", Dh);
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0) return MIT_OK;
   AttnK a = make_k(x);

@@ -127,6 +127,17 @@ __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
 
 // error plumbing shared by every C-ABI entry point (capi.cpp)
 int mit_set_error(const char* fmt, ...);
+
+// launch-plan recording (capi.cpp, mit_plan_*): while a plan records, every launching entry point
+// appends a replay closure (arguments copied by value) and then runs normally, so the recorded step
+// is a real step and argument errors surface at record time.
+#include <functional>
+bool mit_plan_recording();
+void mit_plan_push(std::function<int()> op);
+#define MIT_RECORD(...)                                \
+  do {                                                 \
+    if (mit_plan_recording()) mit_plan_push(__VA_ARGS__); \
+  } while (0)
 #define MIT_CHECK_ARG(cond, ...)          \
   do {                                    \
     if (!(cond)) {                        \

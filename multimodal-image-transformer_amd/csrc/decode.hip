@@ -244,6 +244,7 @@ extern "C" int mit_attention_decode(int dtype, long B, long H, long Dh, const vo
                                     long k_row, long k_batch, const void* v, long v_row, long v_batch, void* o,
                                     long o_batch, long Lk, const int64_t* pos, const int64_t* key_tokens,
                                     long tok_batch, int pad_idx, float scale, void* stream) {
+  MIT_RECORD([=]() { return mit_attention_decode(dtype, B, H, Dh, q, q_batch, k, k_row, k_batch, v, v_row, v_batch, o, o_batch, Lk, pos, key_tokens, tok_batch, pad_idx, scale, stream); });
   MIT_CHECK_ARG(q && k && v && o, "mit_attention_decode: null pointer");
   MIT_CHECK_ARG(Dh == 16 || Dh == 32 || Dh == 64 || Dh == 128, "mit_attention_decode: head_dim %ld unsupported", Dh);
   MIT_CHECK_ARG(dtype == MIT_BF16 || dtype == MIT_F32, "mit_attention_decode: bad dtype");
@@ -272,6 +273,7 @@ extern "C" int mit_attention_decode(int dtype, long B, long H, long Dh, const vo
 
 extern "C" int mit_kv_store(int dtype, long B, long n, const void* src, long s_batch, void* cache, long c_row,
                             long c_batch, const int64_t* pos, void* stream) {
+  MIT_RECORD([=]() { return mit_kv_store(dtype, B, n, src, s_batch, cache, c_row, c_batch, pos, stream); });
   MIT_CHECK_ARG(src && cache && pos, "mit_kv_store: null pointer");
   if (B <= 0 || n <= 0) return MIT_OK;
   DISPATCH_DT(dtype, hipLaunchKernelGGL(kv_store_kernel<T>, dim3(grid_for(B * n)), dim3(256), 0, (hipStream_t)stream,
@@ -282,6 +284,7 @@ extern "C" int mit_kv_store(int dtype, long B, long n, const void* src, long s_b
 
 extern "C" int mit_embed_decode(int dtype, long B, long d, const int64_t* ids, long ld_ids, const int64_t* pos,
                                 const void* table, float scale, const float* pe, void* out, void* stream) {
+  MIT_RECORD([=]() { return mit_embed_decode(dtype, B, d, ids, ld_ids, pos, table, scale, pe, out, stream); });
   MIT_CHECK_ARG(ids && pos && table && pe && out, "mit_embed_decode: null pointer");
   if (B <= 0) return MIT_OK;
   DISPATCH_DT(dtype, hipLaunchKernelGGL(embed_decode_kernel<T>, dim3(grid_for(B * d)), dim3(256), 0,
@@ -294,6 +297,7 @@ extern "C" int mit_embed_decode(int dtype, long B, long d, const int64_t* ids, l
 extern "C" int mit_greedy_pick(long B, long V, const float* logits, long ld, int64_t* ids, long ld_ids,
                                const int64_t* pos, int64_t end_id, int64_t pad_id, int* finished, int* n_finished,
                                void* stream) {
+  MIT_RECORD([=]() { return mit_greedy_pick(B, V, logits, ld, ids, ld_ids, pos, end_id, pad_id, finished, n_finished, stream); });
   MIT_CHECK_ARG(logits && ids && pos && finished && n_finished && ld >= V && V > 0, "mit_greedy_pick: bad arguments");
   if (B <= 0) return MIT_OK;
   hipLaunchKernelGGL(greedy_pick_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, V, logits, ld, ids,

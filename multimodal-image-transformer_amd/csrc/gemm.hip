@@ -1107,6 +1107,7 @@ extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
 
 extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   MIT_CHECK_ARG(g != nullptr, "mit_gemm: null args");
+  MIT_RECORD([c = *g, stream]() { return mit_gemm(&c, stream); });
   MIT_CHECK_ARG(g->dtype == MIT_F32 || g->dtype == MIT_BF16, "mit_gemm: bad dtype %d", g->dtype);
   MIT_CHECK_ARG(g->M >= 0 && g->N >= 0 && g->K >= 0, "mit_gemm: negative extent");
   MIT_CHECK_ARG(g->A && g->B && g->C, "mit_gemm: null operand");

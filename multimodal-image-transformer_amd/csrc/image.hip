@@ -43,6 +43,11 @@ __global__ __launch_bounds__(256) void normalize_u8_kernel(long npix4, long hw, 
 
 extern "C" int mit_image_normalize(long B, long H, long W, const uint8_t* src, float* dst, const float* mean3,
                                    const float* std3, void* stream) {
+  MIT_CHECK_ARG(mean3 && std3, "mit_image_normalize: null mean/std");
+  MIT_RECORD([=, m0 = mean3[0], m1 = mean3[1], m2 = mean3[2], s0 = std3[0], s1 = std3[1], s2 = std3[2]]() {
+    const float m[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
+    return mit_image_normalize(B, H, W, src, dst, m, sd, stream);
+  });
   MIT_CHECK_ARG(src && dst && mean3 && std3, "mit_image_normalize: null pointer");
   MIT_CHECK_ARG(B >= 0 && H > 0 && W > 0, "mit_image_normalize: bad extent");
   MIT_CHECK_ARG((H * W) % 4 == 0, "mit_image_normalize: H*W must be a multiple of 4");

@@ -119,77 +119,85 @@ __global__ void embed_bwd_kernel(long B, long T_, long d, const int64_t* __restr
 
 // Deterministic embedding backward (replaces the float atomics above): the gradient row of token v
 // is the sum over the positions holding v, taken in a FIXED order. Plan (depends on the tokens
-// only): rank_i = #{j: tok_j < tok_i} + #{j < i: tok_j == tok_i} is position i's slot in the
-// (token, position)-sorted order; plan[rank_i] = i, and the first position of every token records
-// its segment length and start. One 64-thread block per 64 positions, tokens staged in LDS tiles.
-__global__ __launch_bounds__(64) void embed_plan_kernel(const int64_t* __restrict__ tok, int n, int* __restrict__ plan) {
-  __shared__ int64_t ts[64];
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  const int64_t ti = i < n ? tok[i] : 0;
-  int less = 0, eq_before = 0, eq = 0;
-  for (int j0 = 0; j0 < n; j0 += 64) {
-    __syncthreads();
-    if (j0 + (int)threadIdx.x < n) ts[threadIdx.x] = tok[j0 + threadIdx.x];
-    __syncthreads();
-    const int nj = min(64, n - j0);
-    for (int jj = 0; jj < nj; ++jj) {
-      const int64_t t = ts[jj];
-      const int e = t == ti;
-      less += t < ti;
-      eq += e;
-      eq_before += e & (j0 + jj < i);
+// only): ONE workgroup bitonic-sorts the (token << 20 | position) keys in LDS (n <= 16384, so the
+// step's 4032 positions sort in 78 compare-exchange stages of one block), then plan[k] = position
+// of sorted slot k and plan[n + k] = the length of the token's run starting at k (0 if slot k is not
+// the first of its token).
+constexpr int EMB_PLAN_MAX = 16384;
+__global__ __launch_bounds__(1024) void embed_plan_kernel(const int64_t* __restrict__ tok, int n, int npow2,
+                                                          int* __restrict__ plan) {
+  extern __shared__ uint64_t keys[];
+  for (int i = threadIdx.x; i < npow2; i += 1024)
+    keys[i] = i < n ? ((uint64_t)tok[i] << 20) | (uint64_t)i : ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= npow2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < npow2; i += 1024) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t x = keys[i], y = keys[ixj];
+          if ((x > y) == ((i & k) == 0)) {
+            keys[i] = y;
+            keys[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
     }
-  }
-  if (i < n) {
-    const int rank = less + eq_before;
-    plan[rank] = i;
-    plan[n + i] = eq_before == 0 ? eq : 0;  // segment head: its length, else 0
-    plan[2 * n + i] = rank;                 // segment start (sorted slot of the head)
+  for (int k = threadIdx.x; k < n; k += 1024) {
+    const uint64_t t = keys[k] >> 20;
+    plan[k] = (int)(keys[k] & 0xFFFFFu);
+    int len = 0;
+    if (k == 0 || (keys[k - 1] >> 20) != t) {
+      len = 1;
+      while (k + len < n && (keys[k + len] >> 20) == t) ++len;
+    }
+    plan[n + k] = len;
   }
 }
 
-// one block per position; the head of each token's segment sums the segment's dx rows: wave w takes
-// rows w, w+4, ... in sorted (= position) order, the 4 wave partials are added in wave order, and the
-// row is STORED (dtable is zeroed once before; PAD's row receives nothing). d <= 1024.
+// one wave per sorted slot; the first slot of each token's run sums the run's dx rows in position
+// order (each lane owns 8 consecutive columns per 512) and STORES the row (dtable is zeroed once
+// before; PAD's row receives nothing). d % 8 == 0.
 template <typename T>
 __global__ __launch_bounds__(256) void embed_bwd_seg_kernel(int n, int d, const int64_t* __restrict__ tok,
                                                             const T* __restrict__ dx, float scale,
                                                             const uint64_t* seed, uint32_t site, uint32_t thresh,
                                                             float dscale, int dropout, int pad,
                                                             const int* __restrict__ plan, float* __restrict__ dtable) {
-  __shared__ float part[4][1024];
-  const int i = blockIdx.x;
-  const int len = plan[n + i];
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= n) return;
+  const int len = plan[n + k];
   if (len == 0) return;
-  const int64_t id = tok[i];
+  const int* perm = plan + k;
+  const int64_t id = tok[perm[0]];
   if (id == pad) return;
-  const int* perm = plan + plan[2 * n + i];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   const uint64_t key = dropout ? site_key(seed, site) : 0ull;
-  float acc[16];
+  for (int c0 = lane * 8; c0 < d; c0 += 512) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < len; ++r) {
+      const long j = perm[r];
+      float v[8];
+      if constexpr (sizeof(T) == 2) {
+        const bf16x8 x = *(const bf16x8*)(dx + j * d + c0);
 #pragma unroll
-  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-  for (int k = w; k < len; k += 4) {
-    const long j = perm[k];
-    const T* row = dx + j * d;
+        for (int q = 0; q < 8; ++q) v[q] = (float)x[q];
+      } else {
+        const f32x4 x0 = *(const f32x4*)(dx + j * d + c0), x1 = *(const f32x4*)(dx + j * d + c0 + 4);
+        v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3]; v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
+      }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int c = lane + 64 * q;
-      if (c < d) {
-        float g = to_f(row[c]) * scale;
-        if (dropout) g *= drop_mul(key, (uint64_t)(j * d + c), thresh, dscale);
+      for (int q = 0; q < 8; ++q) {
+        float g = v[q] * scale;
+        if (dropout) g *= drop_mul(key, (uint64_t)(j * d + c0 + q), thresh, dscale);
         acc[q] += g;
       }
     }
+    f32x4* o = (f32x4*)(dtable + id * d + c0);
+    o[0] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    o[1] = f32x4{acc[4], acc[5], acc[6], acc[7]};
   }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int c = lane + 64 * q;
-    if (c < d) part[w][c] = acc[q];
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < d; c += 256)
-    dtable[id * d + c] = ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -452,6 +460,7 @@ inline unsigned grid_for(long n, int block = 256, long cap = 8192) {
 
 extern "C" int mit_im2col(int dtype, long B, long C, long H, long W, long P, const float* img, void* out, long kpad,
                           void* stream) {
+  MIT_RECORD([=]() { return mit_im2col(dtype, B, C, H, W, P, img, out, kpad, stream); });
   MIT_CHECK_ARG(img && out && P > 0 && H % P == 0 && W % P == 0 && kpad >= C * P * P, "mit_im2col: bad arguments");
   const long total = B * (H / P) * (W / P) * kpad;
   if (dtype == MIT_BF16 && P % 8 == 0 && W % 4 == 0 && kpad % 8 == 0 && ((uintptr_t)img % 16) == 0 &&
@@ -469,6 +478,7 @@ extern "C" int mit_im2col(int dtype, long B, long C, long H, long W, long P, con
 
 extern "C" int mit_vit_assemble(int dtype, long B, long np, long E, const void* patch, const float* cls,
                                 const float* pos, void* h, void* stream) {
+  MIT_RECORD([=]() { return mit_vit_assemble(dtype, B, np, E, patch, cls, pos, h, stream); });
   MIT_CHECK_ARG(patch && cls && pos && h, "mit_vit_assemble: null pointer");
   const long total = B * (np + 1) * E;
   if (dtype == MIT_BF16 && E % 8 == 0 && ((uintptr_t)patch % 16) == 0 && ((uintptr_t)h % 16) == 0 &&
@@ -487,6 +497,7 @@ extern "C" int mit_vit_assemble(int dtype, long B, long np, long E, const void* 
 extern "C" int mit_embed_fwd(int dtype, long B, long T_, long d, const int64_t* tokens, const void* table, float scale,
                              const float* pe, float drop_p, const uint64_t* seed, uint32_t site, void* out,
                              void* stream) {
+  MIT_RECORD([=]() { return mit_embed_fwd(dtype, B, T_, d, tokens, table, scale, pe, drop_p, seed, site, out, stream); });
   MIT_CHECK_ARG(tokens && table && pe && out, "mit_embed_fwd: null pointer");
   const long total = B * T_ * d;
   const int dropout = drop_p > 0.f;
@@ -499,13 +510,22 @@ extern "C" int mit_embed_fwd(int dtype, long B, long T_, long d, const int64_t* 
   return MIT_OK;
 }
 
-extern "C" long mit_embed_plan_ints(long n) { return 3 * n; }
+extern "C" long mit_embed_plan_ints(long n) { return 2 * n; }
 
 extern "C" int mit_embed_plan(const int64_t* tokens, long n, int* plan, void* stream) {
-  MIT_CHECK_ARG(tokens && plan && n >= 0 && n < (1L << 30), "mit_embed_plan: bad arguments");
+  MIT_RECORD([=]() { return mit_embed_plan(tokens, n, plan, stream); });
+  MIT_CHECK_ARG(tokens && plan && n >= 0 && n <= EMB_PLAN_MAX, "mit_embed_plan: n = %ld positions (max %d)", n,
+                EMB_PLAN_MAX);
   if (n == 0) return MIT_OK;
-  hipLaunchKernelGGL(embed_plan_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, tokens,
-                     (int)n, plan);
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)embed_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              EMB_PLAN_MAX * 8);
+    attr = true;
+  }
+  hipLaunchKernelGGL(embed_plan_kernel, dim3(1), dim3(1024), np2 * 8, (hipStream_t)stream, tokens, (int)n, np2, plan);
   MIT_LAUNCH_CHECK("mit_embed_plan");
   return MIT_OK;
 }
@@ -513,15 +533,18 @@ extern "C" int mit_embed_plan(const int64_t* tokens, long n, int* plan, void* st
 extern "C" int mit_embed_bwd(int dtype, long B, long T_, long d, const int64_t* tokens, const void* dx, float scale,
                              float drop_p, const uint64_t* seed, uint32_t site, int pad_idx, const int* plan,
                              float* dtable, void* stream) {
+  MIT_RECORD([=]() { return mit_embed_bwd(dtype, B, T_, d, tokens, dx, scale, drop_p, seed, site, pad_idx, plan, dtable, stream); });
   MIT_CHECK_ARG(tokens && dx && dtable, "mit_embed_bwd: null pointer");
   const long total = B * T_ * d;
   const int dropout = drop_p > 0.f;
   const uint32_t th = drop_threshold(drop_p);
   const float sc = drop_p < 1.f ? 1.f / (1.f - drop_p) : 0.f;
   if (plan) {
-    MIT_CHECK_ARG(d <= 1024 && B * T_ < (1L << 30), "mit_embed_bwd: the deterministic path takes d <= 1024");
+    MIT_CHECK_ARG(d % 8 == 0 && B * T_ <= EMB_PLAN_MAX && ((uintptr_t)dx % 16) == 0 && ((uintptr_t)dtable % 16) == 0,
+                  "mit_embed_bwd: the deterministic path takes d %% 8 == 0, <= %d positions, 16-B aligned rows",
+                  EMB_PLAN_MAX);
     if (B * T_ == 0) return MIT_OK;
-    DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_seg_kernel<T>, dim3((unsigned)(B * T_)), dim3(256), 0,
+    DISPATCH_T(dtype, hipLaunchKernelGGL(embed_bwd_seg_kernel<T>, dim3((unsigned)((B * T_ + 3) / 4)), dim3(256), 0,
                                          (hipStream_t)stream, (int)(B * T_), (int)d, tokens, (const T*)dx, scale, seed,
                                          site, th, sc, dropout, pad_idx, plan, dtable));
     MIT_LAUNCH_CHECK("mit_embed_bwd");
@@ -535,6 +558,7 @@ extern "C" int mit_embed_bwd(int dtype, long B, long T_, long d, const int64_t* 
 }
 
 extern "C" int mit_count_targets(const int64_t* targets, long n, int ignore_index, float* count, void* stream) {
+  MIT_RECORD([=]() { return mit_count_targets(targets, n, ignore_index, count, stream); });
   MIT_CHECK_ARG(targets && count, "mit_count_targets: null pointer");
   if (n <= 0) return MIT_OK;
   hipLaunchKernelGGL(count_kernel, dim3(grid_for(n, 256, 64)), dim3(256), 0, (hipStream_t)stream, targets, n,
@@ -546,6 +570,7 @@ extern "C" int mit_count_targets(const int64_t* targets, long n, int ignore_inde
 extern "C" int mit_cross_entropy(int dtype, long rows, long V, void* logits, long ld, const int64_t* targets,
                                  int ignore_index, const float* count, float* loss_sum, int want_grad,
                                  float* row_loss, void* stream) {
+  MIT_RECORD([=]() { return mit_cross_entropy(dtype, rows, V, logits, ld, targets, ignore_index, count, loss_sum, want_grad, row_loss, stream); });
   MIT_CHECK_ARG(logits && targets && loss_sum && (!want_grad || count), "mit_cross_entropy: null pointer");
   MIT_CHECK_ARG(ld >= V, "mit_cross_entropy: ld < V");
   if (rows <= 0) return MIT_OK;
@@ -573,6 +598,7 @@ extern "C" long mit_colsum_ws_floats(long M, long N) { return ((M + CS_ROWS - 1)
 
 extern "C" int mit_colsum(int dtype, long M, long N, const void* dy, long ld, float* out, int accumulate, float* ws,
                           void* stream) {
+  MIT_RECORD([=]() { return mit_colsum(dtype, M, N, dy, ld, out, accumulate, ws, stream); });
   MIT_CHECK_ARG(dy && out && ws && ld >= N, "mit_colsum: bad arguments");
   if (N <= 0) return MIT_OK;
   const long nch = (M + CS_ROWS - 1) / CS_ROWS;
@@ -590,6 +616,7 @@ extern "C" int mit_colsum(int dtype, long M, long N, const void* dy, long ld, fl
 extern "C" long mit_grad_norm_ws_floats(long n) { (void)n; return GN_BLOCKS; }
 
 extern "C" int mit_grad_norm(const float* grads, long n, float max_norm, float* ws, float* norm_out, void* stream) {
+  MIT_RECORD([=]() { return mit_grad_norm(grads, n, max_norm, ws, norm_out, stream); });
   MIT_CHECK_ARG(grads && ws && norm_out, "mit_grad_norm: null pointer");
   MIT_CHECK_ARG(((uintptr_t)grads % 16) == 0, "mit_grad_norm: grads must be 16-B aligned");
   hipStream_t s = (hipStream_t)stream;
@@ -601,6 +628,7 @@ extern "C" int mit_grad_norm(const float* grads, long n, float max_norm, float* 
 }
 
 extern "C" int mit_step_inc(int64_t* step, void* stream) {
+  MIT_RECORD([=]() { return mit_step_inc(step, stream); });
   MIT_CHECK_ARG(step, "mit_step_inc: null pointer");
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step);
   MIT_LAUNCH_CHECK("mit_step_inc");
@@ -610,6 +638,7 @@ extern "C" int mit_step_inc(int64_t* step, void* stream) {
 extern "C" int mit_adamw(long n, float* param, const float* grad, float* m, float* v, void* shadow_bf16,
                          const float* norm_out, const float* lr, const int64_t* step, float beta1, float beta2,
                          float eps, float weight_decay, void* stream) {
+  MIT_RECORD([=]() { return mit_adamw(n, param, grad, m, v, shadow_bf16, norm_out, lr, step, beta1, beta2, eps, weight_decay, stream); });
   MIT_CHECK_ARG(param && grad && m && v && lr && step, "mit_adamw: null pointer");
   MIT_CHECK_ARG(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                 "mit_adamw: buffers must be 16-B aligned");
@@ -628,6 +657,7 @@ extern "C" int mit_adamw(long n, float* param, const float* grad, float* m, floa
 }
 
 extern "C" int mit_cast_f32(int dtype, long n, const float* src, void* dst, void* stream) {
+  MIT_RECORD([=]() { return mit_cast_f32(dtype, n, src, dst, stream); });
   MIT_CHECK_ARG(src && dst, "mit_cast_f32: null pointer");
   if (n <= 0) return MIT_OK;
   DISPATCH_T(dtype, hipLaunchKernelGGL(cast_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, src,
@@ -637,6 +667,7 @@ extern "C" int mit_cast_f32(int dtype, long n, const float* src, void* dst, void
 }
 
 extern "C" int mit_dropout_mask(long n, float p, const uint64_t* seed, uint32_t site, float* out, void* stream) {
+  MIT_RECORD([=]() { return mit_dropout_mask(n, p, seed, site, out, stream); });
   MIT_CHECK_ARG(out, "mit_dropout_mask: null pointer");
   if (n <= 0) return MIT_OK;
   const float sc = p < 1.f ? 1.f / (1.f - p) : 0.f;
@@ -647,6 +678,7 @@ extern "C" int mit_dropout_mask(long n, float p, const uint64_t* seed, uint32_t 
 }
 
 extern "C" int mit_scalar_div(const float* a, const float* b, float* out, void* stream) {
+  MIT_RECORD([=]() { return mit_scalar_div(a, b, out, stream); });
   MIT_CHECK_ARG(a && b && out, "mit_scalar_div: null pointer");
   hipLaunchKernelGGL(scalar_div_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, a, b, out);
   MIT_LAUNCH_CHECK("mit_scalar_div");
@@ -654,6 +686,7 @@ extern "C" int mit_scalar_div(const float* a, const float* b, float* out, void* 
 }
 
 extern "C" int mit_zero(void* p, long bytes, void* stream) {
+  MIT_RECORD([=]() { return mit_zero(p, bytes, stream); });
   MIT_CHECK_ARG(p || bytes == 0, "mit_zero: null pointer");
   if (bytes <= 0) return MIT_OK;
   hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);

@@ -294,6 +294,7 @@ extern "C" int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x,
                                  float r_drop_p, const uint64_t* seed, uint32_t site, const float* gamma,
                                  const float* beta, float eps, void* z, void* y, long ldy, float* mean, float* rstd,
                                  void* stream) {
+  MIT_RECORD([=]() { return mit_layernorm_fwd(dtype, rows, cols, x, ldx, r, ldr, r_drop_p, seed, site, gamma, beta, eps, z, y, ldy, mean, rstd, stream); });
   MIT_CHECK_ARG(cols > 0 && cols <= 64 * MAXV_ALL, "mit_layernorm_fwd: cols %ld out of range", cols);
   MIT_CHECK_ARG(x && y && gamma && beta, "mit_layernorm_fwd: null pointer");
   MIT_CHECK_ARG(ldx >= cols && ldy >= cols && (!r || ldr >= cols), "mit_layernorm_fwd: bad leading dim");
@@ -336,6 +337,7 @@ extern "C" int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy
                                  const float* rstd, const float* gamma, void* dx, void* dr, float r_drop_p,
                                  const uint64_t* seed, uint32_t site, float* dgamma, float* dbeta, float* ws,
                                  void* stream) {
+  MIT_RECORD([=]() { return mit_layernorm_bwd(dtype, rows, cols, dy, z, mean, rstd, gamma, dx, dr, r_drop_p, seed, site, dgamma, dbeta, ws, stream); });
   MIT_CHECK_ARG(cols > 0 && cols <= 64 * MAXV_ALL, "mit_layernorm_bwd: cols %ld out of range", cols);
   MIT_CHECK_ARG(dy && z && mean && rstd && gamma && dx && ws, "mit_layernorm_bwd: null pointer");
   MIT_CHECK_ARG(!dgamma == !dbeta, "mit_layernorm_bwd: dgamma and dbeta must both be set or both be NULL");
@@ -375,6 +377,7 @@ extern "C" int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy
 
 extern "C" int mit_layernorm_param_grads(long rows, long cols, const float* ws, float* dgamma, float* dbeta,
                                          void* stream) {
+  MIT_RECORD([=]() { return mit_layernorm_param_grads(rows, cols, ws, dgamma, dbeta, stream); });
   MIT_CHECK_ARG(ws && dgamma && dbeta, "mit_layernorm_param_grads: null pointer");
   MIT_CHECK_ARG(cols > 0, "mit_layernorm_param_grads: cols %ld", cols);
   if (rows <= 0) return MIT_OK;

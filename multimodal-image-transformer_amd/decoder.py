@@ -229,13 +229,17 @@ class _SideStream:
 
     def under(self, fn):
         """Run fn (e.g. a DP gradient-bucket all-reduce) on the side stream after everything issued
-        so far on both streams."""
-        self.stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream):
-            fn()
+        so far on both streams (a host step of a recorded program: native.host_call)."""
+        self.events.wait_stream(self.ptr, native.stream_ptr())
+
+        def call():
+            with torch.cuda.stream(self.stream):
+                fn()
+        native.host_call(call)
 
     def join(self):
-        torch.cuda.current_stream().wait_stream(self.stream)
+        """The caller's stream waits for everything issued on the side stream."""
+        native.HipEvents.wait(native.stream_ptr(), self.side_events.record(self.ptr))
         self.pending.clear()
 
 

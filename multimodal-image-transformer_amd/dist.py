@@ -23,6 +23,8 @@ from typing import List
 import torch
 import torch.distributed as dist
 
+import native
+
 
 def init_from_env(backend: str = None):
     """torch.distributed init from RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun)."""
@@ -69,7 +71,7 @@ class DataParallel:
 
     # hooks called by model.train_step ------------------------------------------------------------
     def all_reduce_count(self, count: torch.Tensor):
-        dist.all_reduce(count, group=self.group)
+        native.host_call(lambda: dist.all_reduce(count, group=self.group))
 
     def grads_ready(self, first: str, last: str):
         s, e = self.store.span(first, last)
@@ -79,6 +81,9 @@ class DataParallel:
             self._pending_spans.append((s, e))
 
     def finish_backward(self, loss: torch.Tensor):
+        native.host_call(lambda: self._finish(loss))
+
+    def _finish(self, loss: torch.Tensor):
         if not self.overlap and self._pending_spans:
             s = min(a for a, _ in self._pending_spans)
             e = max(b for _, b in self._pending_spans)

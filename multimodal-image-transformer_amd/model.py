@@ -222,14 +222,15 @@ class ImageToTextModel:
             return
         if self._enc_stream is None:
             self._enc_stream = torch.cuda.Stream(device=self.device)
+            self._enc_events = native.HipEvents(8)
         slot = 1 - self._enc_slot
         images = images.to(self.device, non_blocking=True)
-        main = torch.cuda.current_stream(self.device)
-        self._enc_stream.wait_stream(main)  # the arena's previous reader (two steps back) is done
+        enc = self._enc_stream.cuda_stream
+        # the arena's previous reader (two steps back) is done: the encoder stream waits for main
+        self._enc_events.wait_stream(enc, native.stream_ptr())
         with torch.cuda.stream(self._enc_stream):
             out = self._encoder_rows(images, slot)
-        ev = torch.cuda.Event()
-        ev.record(self._enc_stream)
+        ev = self._enc_events.record(enc)
         self._prefetched = self._last_pf = (images, slot, out, ev)
 
     def _encode_memory(self, images: torch.Tensor):
@@ -242,7 +243,7 @@ class ImageToTextModel:
         pf, self._prefetched = self._prefetched, None
         if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
             _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
-            torch.cuda.current_stream(self.device).wait_event(ev)
+            native.HipEvents.wait(native.stream_ptr(), ev)
         else:
             enc_rows, enc_ld, S = self._encoder_rows(images, self._enc_slot)
         if not self.has_projection:

@@ -94,6 +94,13 @@ SIGNATURES = {
     "mit_kv_store": (I, [I, L, L, vp, L, vp, L, L, vp, vp]),
     "mit_embed_decode": (I, [I, L, L, vp, L, vp, vp, Fl, vp, vp, vp]),
     "mit_image_normalize": (I, [L, L, L, vp, vp, ctypes.POINTER(Fl), ctypes.POINTER(Fl), vp]),
+    "mit_plan_begin": (vp, []),
+    "mit_plan_end": (vp, []),
+    "mit_plan_size": (L, [vp]),
+    "mit_plan_run": (I, [vp]),
+    "mit_plan_destroy": (None, [vp]),
+    "mit_event_record": (I, [vp, vp]),
+    "mit_stream_wait_event": (I, [vp, vp]),
     "mit_greedy_pick": (I, [L, L, vp, L, vp, L, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp]),
 }
 
@@ -166,7 +173,8 @@ class on_stream:
 
 class HipEvents:
     """Timing-free HIP events from a recycled pool, recorded / waited on raw stream pointers
-    (cross-stream edges of the step without torch.cuda.Event's Python overhead)."""
+    (cross-stream edges of the step without torch.cuda.Event's Python overhead). Record and wait go
+    through the library (mit_event_record / mit_stream_wait_event), so launch plans capture them."""
     _hip = None
     DISABLE_TIMING = 0x2
 
@@ -174,8 +182,6 @@ class HipEvents:
         if HipEvents._hip is None:
             h = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded
             h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
-            h.hipEventRecord.argtypes = [vp, vp]
-            h.hipStreamWaitEvent.argtypes = [vp, vp, ctypes.c_uint]
             h.hipEventDestroy.argtypes = [vp]
             HipEvents._hip = h
         self.pool = []
@@ -191,18 +197,80 @@ class HipEvents:
         records: callers wait on an event well before that (one step issues < 64)."""
         ev = self.pool[self.i]
         self.i = (self.i + 1) % len(self.pool)
-        if HipEvents._hip.hipEventRecord(ev, stream) != 0:
-            raise NativeError("hipEventRecord failed")
+        _check(lib().mit_event_record(ev, stream), "mit_event_record")
         return ev
 
     @staticmethod
     def wait(stream, ev):
-        if HipEvents._hip.hipStreamWaitEvent(stream, ev, 0) != 0:
-            raise NativeError("hipStreamWaitEvent failed")
+        _check(lib().mit_stream_wait_event(stream, ev), "mit_stream_wait_event")
 
     def wait_stream(self, stream, other):
         """stream waits for everything issued so far on other."""
         self.wait(stream, self.record(other))
+
+
+# ------------------------------------------------------------------------------------------------
+# recorded programs: native launch plans (mit_plan_*) interleaved with host calls
+# ------------------------------------------------------------------------------------------------
+class Program:
+    """One recorded run of a host function (e.g. a train step + optimizer step): its launches as
+    native plans, cut wherever the function made a host call (host_call: a collective, a Python
+    callback), which is re-run in place. run() replays everything in the recorded order."""
+
+    def __init__(self):
+        self.items = []  # (0, plan handle) | (1, callable)
+
+    def run(self):
+        for kind, x in self.items:
+            if kind == 0:
+                _check(lib().mit_plan_run(x), "mit_plan_run")
+            else:
+                x()
+
+    def launches(self) -> int:
+        return sum(lib().mit_plan_size(x) for k, x in self.items if k == 0)
+
+    def __del__(self):
+        if _lib is not None:
+            for kind, x in self.items:
+                if kind == 0 and x:
+                    _lib.mit_plan_destroy(x)
+        self.items = []
+
+
+_recording: Optional[Program] = None
+
+
+def record(fn) -> Program:
+    """Run fn() once for real while recording every native launch (and host_call) into a Program."""
+    global _recording
+    if _recording is not None:
+        raise NativeError("record: already recording")
+    prog = Program()
+    if not lib().mit_plan_begin():
+        raise NativeError(f"mit_plan_begin failed: {lib().mit_last_error().decode()}")
+    _recording = prog
+    try:
+        fn()
+    finally:
+        prog.items.append((0, lib().mit_plan_end()))
+        _recording = None
+    return prog
+
+
+def host_call(fn):
+    """Run a host-side action now; inside record(), also record it as a host step of the Program
+    between two native plans (so a replay re-runs it at the same point of the launch sequence)."""
+    if _recording is not None:
+        _recording.items.append((0, lib().mit_plan_end()))
+        _recording.items.append((1, fn))
+        try:
+            fn()
+        finally:
+            if not lib().mit_plan_begin():
+                raise NativeError(f"mit_plan_begin failed: {lib().mit_last_error().decode()}")
+        return
+    fn()
 
 
 def dtype_code(t: torch.Tensor) -> int:

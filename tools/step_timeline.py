@@ -1,0 +1,57 @@
+"""Concurrency timeline of ONE train step from a rocprofv3 --kernel-trace CSV (eager bench run; the
+step = dispatches between the last two AdamW launches): wall, time with 0 / 1 / 2 / 3+ kernels in
+flight, per-queue busy time, and per kernel family the time it ran ALONE (nothing else on the chip:
+the critical-path suspects). Usage: python tools/step_timeline.py kernel_trace.csv"""
+import collections
+import csv
+import sys
+
+from trace_step import short
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ad = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
+    a, b = ad[-2] + 1, ad[-1] + 1
+    step = rows[a:b]
+    t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
+    ev = []
+    for i, r in enumerate(step):
+        ev.append((int(r["Start_Timestamp"]), 1, i))
+        ev.append((int(r["End_Timestamp"]), -1, i))
+    ev.sort()
+    active = set()
+    hist = collections.Counter()
+    alone = collections.Counter()
+    last = t0
+    for t, kind, i in ev:
+        dt = t - last
+        if dt > 0:
+            hist[min(len(active), 3)] += dt
+            if len(active) == 1:
+                (only,) = tuple(active)
+                alone[short(step[only]["Kernel_Name"])] += dt
+        last = t
+        if kind == 1:
+            active.add(i)
+        else:
+            active.discard(i)
+    wall = t1 - t0
+    qkey = "Queue_Id" if "Queue_Id" in step[0] else ("Stream_Id" if "Stream_Id" in step[0] else None)
+    print(f"one step: {len(step)} dispatches, wall {wall / 1e3:.1f} us")
+    print("  in flight: " + ", ".join(f"{k}{'+' if k == 3 else ''}: {hist[k] / 1e3:.1f} us ({100 * hist[k] / wall:.1f}%)"
+                                      for k in range(4)))
+    if qkey:
+        q = collections.Counter()
+        for r in step:
+            q[r[qkey]] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        for k, v in sorted(q.items()):
+            print(f"  {qkey} {k}: kernel time {v / 1e3:.1f} us")
+    print("ran alone (us):")
+    for k, v in alone.most_common(25):
+        print(f"  {v / 1e3:8.1f}  {k}")
+
+
+if __name__ == "__main__":
+    main()
