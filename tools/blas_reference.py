@@ -1,0 +1,79 @@
+"""Per-shape GEMM time: mit_gemm (our kernels) vs torch.matmul (hipBLASLt, the vendor library as a
+known-good reference on the same device; guide §5.4 rule 10), bf16, random operands, interleaved
+rounds in one process. Shapes = the configs[1] train step's GEMMs (encoder B*197 = 12608 rows,
+decoder B*T = 4032 rows). Usage (GPU box): python tools/blas_reference.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-image-transformer_amd"))
+import torch  # noqa: E402
+
+import native  # noqa: E402
+
+# name, M, N, K, a_layout, b_layout (0 = K-contig, 1 = MN-contig), count per step
+SHAPES = [
+    ("enc qkv", 12608, 2304, 768, 0, 0, 12), ("enc o+res", 12608, 768, 768, 0, 0, 12),
+    ("enc fc1+gelu", 12608, 3072, 768, 0, 0, 12), ("enc fc2+res", 12608, 768, 3072, 0, 0, 12),
+    ("dec kv_all", 12608, 6144, 512, 0, 0, 1), ("dec self_in", 4032, 1536, 512, 0, 0, 6),
+    ("dec d-out", 4032, 512, 512, 0, 0, 18), ("dec ffn1", 4032, 2048, 512, 0, 0, 6),
+    ("dec ffn2", 4032, 512, 2048, 0, 0, 6), ("dec fc_out", 4032, 10000, 512, 0, 0, 1),
+    ("dX d-out", 4032, 512, 512, 0, 1, 18), ("dX ffn1", 4032, 512, 2048, 0, 1, 6),
+    ("dX ffn2", 4032, 2048, 512, 0, 1, 6), ("dX self_in", 4032, 512, 1536, 0, 1, 6),
+    ("dX fc_out", 4032, 512, 10000, 0, 1, 1), ("dX kv_all", 12608, 512, 6144, 0, 1, 1),
+    ("dW d-d", 512, 512, 4032, 1, 1, 18), ("dW ffn1", 2048, 512, 4032, 1, 1, 6),
+    ("dW ffn2", 512, 2048, 4032, 1, 1, 6), ("dW self_in", 1536, 512, 4032, 1, 1, 6),
+    ("dW fc_out", 10000, 512, 4032, 1, 1, 1), ("dW kv_all", 6144, 512, 12608, 1, 1, 1),
+    ("4096^3", 4096, 4096, 4096, 0, 0, 0),
+]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters  # us
+
+
+def main():
+    native.load_library()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    tot_ours = tot_blas = 0.0
+    print(f"{'shape':14s} {'M':>6s} {'N':>6s} {'K':>6s}  {'ours us':>8s} {'TF':>6s}  {'hipBLASLt us':>12s} {'TF':>6s}  ratio")
+    for name, M, N, K, al, bl, cnt in SHAPES:
+        A = (torch.randn(M, K) if al == 0 else torch.randn(K, M)).to(dev, torch.bfloat16)
+        B = (torch.randn(N, K) if bl == 0 else torch.randn(K, N)).to(dev, torch.bfloat16)
+        out_f32 = al == 1
+        C = torch.empty(M, N, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
+        ws = native.gemm_workspace(M, N, K, dev)
+        kw = {}
+        if "res" in name:
+            kw["residual"] = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        if "gelu" in name:
+            kw["act"] = native.ACT_GELU
+        ours = lambda: native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, workspace=ws, **kw)  # noqa: E731
+        At = A if al == 0 else A.t()
+        Bt = B.t() if bl == 0 else B
+        blas = lambda: torch.matmul(At, Bt)  # noqa: E731
+        to, tb = [], []
+        for _ in range(3):  # interleaved rounds
+            to.append(timeit(ours))
+            tb.append(timeit(blas))
+        to, tb = min(to), min(tb)
+        fl = 2.0 * M * N * K
+        tot_ours += cnt * to
+        tot_blas += cnt * tb
+        print(f"{name:14s} {M:6d} {N:6d} {K:6d}  {to:8.1f} {fl / to / 1e6:6.0f}  {tb:12.1f} {fl / tb / 1e6:6.0f}  {tb / to:5.2f}",
+              flush=True)
+    print(f"per-step GEMM sum (isolated, x count): ours {tot_ours / 1e3:.3f} ms, hipBLASLt {tot_blas / 1e3:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
