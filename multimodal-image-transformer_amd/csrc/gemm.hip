@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "common.h"
 
@@ -145,6 +146,77 @@ __device__ __forceinline__ void epi_row8(const Epi& e, void* C, long ldc, long N
   } else {
     for (int k = 0; k < 8; ++k)
       if (gc + k < N) epi_store<bf16>(e, C, ldc, N, gr, gc + k, v[k]);
+  }
+}
+
+// ---- gathered epilogue: every operand load of a tile's epilogue issued before its first store ----
+// On gfx9 vmcnt counts stores as well as loads, so a load issued after a store is waited for
+// together with that store: an epilogue that loads bias / residual per row segment between its
+// stores serialises one store round trip per segment (7-35 us per launch of the 256 kernel on the
+// encoder shapes). The gathered form loads the bias of the thread's fixed columns once and the
+// residual (or aux mask) of all its segments, then only computes and stores. It covers every
+// epilogue except residual AND aux together, f32 accumulate and the non-vector (ragged ldc)
+// case, which keep the per-segment form (epi_row8).
+__device__ __forceinline__ bool epi_gatherable(const Epi& e) { return e.vec && !(e.res && e.aux) && !e.accumulate; }
+__device__ __forceinline__ void epi_bias8(const Epi& e, long c, long N, float* b) {
+  if (e.bias && c < N) {
+    const f32x4 b0 = *(const f32x4*)(e.bias + c), b1 = *(const f32x4*)(e.bias + c + 4);
+    b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; b[3] = b0[3]; b[4] = b1[0]; b[5] = b1[1]; b[6] = b1[2]; b[7] = b1[3];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = 0.f;
+  }
+}
+// the residual (or aux) segment of row r, columns [c, c+8); zeros when absent / out of range
+__device__ __forceinline__ bf16x8 epi_x8(const Epi& e, long M, long N, long r, long c) {
+  bf16x8 x = {};
+  const bf16* src = (const bf16*)(e.res ? e.res : e.aux);
+  if (src && r < M && c < N) x = *(const bf16x8*)(src + r * (e.res ? e.ldr : e.ld_aux) + c);
+  return x;
+}
+template <bool DROP>
+__device__ __forceinline__ uint64_t epi_key(const Epi& e) {
+  return (DROP && e.dropout) ? site_key(e.seed, e.site) : 0ull;
+}
+// epi8 with the operands from registers (b: bias of the 8 columns, x: residual or aux segment)
+template <int ACT, bool DROP>
+__device__ __forceinline__ void epi8x(const Epi& e, void* C, long ldc, long N, long r, long c, float* v, const float* b,
+                                      bf16x8 x, uint64_t key) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = v[k] * e.alpha + b[k];
+  if (ACT == MIT_ACT_GELU) {
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+      const f32x2 g = gelu_fast2(f32x2{v[k], v[k + 1]});
+      v[k] = g[0];
+      v[k + 1] = g[1];
+    }
+  } else if (ACT != MIT_ACT_NONE) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = act_apply<ACT, true>(e.act, v[k]);
+  }
+  if (e.aux) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= ((float)x[k] > 0.0f) ? e.aux_scale : 0.0f;
+  }
+  if (DROP && e.dropout) {
+    const uint64_t base = (uint64_t)r * (uint64_t)N + (uint64_t)c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= drop_mul(key, base + k, e.thresh, e.dscale);
+  }
+  if (e.res) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += (float)x[k];
+  }
+  if (e.out_f32) {
+    f32x4* o = (f32x4*)((float*)C + r * ldc + c);
+    o[0] = f32x4{v[0], v[1], v[2], v[3]};
+    o[1] = f32x4{v[4], v[5], v[6], v[7]};
+  } else {
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+    *(bf16x8*)((bf16*)C + r * ldc + c) = o;
   }
 }
 
@@ -387,6 +459,26 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     __syncthreads();
     if (!*flag) return;
   }
+  if (!tile_cnt && ksplit == 1 && epi_gatherable(e)) {  // gathered epilogue: all loads, then all stores
+    constexpr int NP = (BM * BN / 8) / 256;
+    const long gc = n0 + (tid & 15) * 8;  // this thread's columns are the same in every pass
+    float b[8];
+    epi_bias8(e, gc, N, b);
+    bf16x8 xs[NP];
+#pragma unroll
+    for (int pass = 0; pass < NP; ++pass) xs[pass] = epi_x8(e, M, N, m0 + ((pass * 256 + tid) >> 4), gc);
+    const uint64_t key = epi_key<DROP>(e);
+#pragma unroll
+    for (int pass = 0; pass < NP; ++pass) {
+      const int r = (pass * 256 + tid) >> 4, c8 = (tid & 15) * 8;
+      const long gr = m0 + r;
+      if (gr >= M || gc >= N) continue;
+      const f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v, b, xs[pass], key);
+    }
+    return;
+  }
 #pragma unroll 2
   for (int pass = 0; pass < (BM * BN / 8) / 256; ++pass) {
     const int id = pass * 256 + tid;
@@ -517,6 +609,12 @@ __device__ __forceinline__ void bar_raw() {
 #endif
 #ifndef MIT_G256_EARLY_A1
 #define MIT_G256_EARLY_A1 1
+#endif
+#ifndef MIT_G256_NOEPI
+#define MIT_G256_NOEPI 0
+#endif
+#ifndef MIT_G256P_SWAP
+#define MIT_G256P_SWAP 1
 #endif
 #ifndef MIT_G256_PRIO  // raise the wave priority around each MFMA block
 #define MIT_G256_PRIO 1
@@ -755,7 +853,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   }
 
   // ---- epilogue: per wave, two passes of 64 rows x 64 cols through a private fp32 LDS stage ----
+#if MIT_G256_NOEPI  // timing experiment only: no output
+  if (acc[0][0][0] != 1234.5f || acc[7][3][3] != 1234.5f) return;
+#endif
   float* cs = (float*)smem + wid * 64 * EPI_LD;
+  const bool gather = ksplit == 1 && epi_gatherable(e);
+  const long gcw = n0 + wc * 64 + (lane & 7) * 8;  // this lane's columns in every pass / row
+  float bw[8];
+  uint64_t key = 0;
+  if (gather) {
+    epi_bias8(e, gcw, N, bw);
+    key = epi_key<DROP>(e);
+  }
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
@@ -766,6 +875,22 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
         for (int t = 0; t < 4; ++t)
           cs[(i * 16 + (lane >> 4) * 4 + t) * EPI_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][t];
     __builtin_amdgcn_wave_barrier();
+    if (gather) {  // this pass's residual / aux segments first, then only stores
+      bf16x8 xs[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it) xs[it] = epi_x8(e, M, N, m0 + wr * 128 + pass * 64 + it * 8 + (lane >> 3), gcw);
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int r = it * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+        const long gr = m0 + wr * 128 + pass * 64 + r;
+        if (gr >= M || gcw >= N) continue;
+        const f32x4 lo = *(const f32x4*)(cs + r * EPI_LD + c8), hi = *(const f32x4*)(cs + r * EPI_LD + c8 + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        epi8x<ACT, DROP>(e, C, ldc, N, gr, gcw, v, bw, xs[it], key);
+      }
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
 #pragma unroll 2
     for (int it = 0; it < 8; ++it) {
       const int id = it * 64 + lane;
@@ -784,6 +909,334 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     }
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Persistent 256x256 kernel (NT / NN with K-contig A, K a multiple of 128). Same tile, waves, LDS
+// images, DMA schedule and 4-barrier-per-K-tile ping-pong as gemm256_kernel, with three changes
+// aimed at the per-tile fixed cost that dominates the encoder's K = 768 shapes (one launch round of
+// the 256 kernel = ~9 us of prologue fill + LDS-staged epilogue + store burst, i.e. 7 K-steps):
+//   * one workgroup per CU walks a list of tiles; the K-tile stream runs on ACROSS tiles, so the
+//     last K-tiles of tile n already DMA tile n+1's first K-tiles (no prologue after the first);
+//   * the MFMA operands are swapped (acc = B-frag x A-frag, i.e. C^T per 16x16 block), so a lane
+//     holds 4 consecutive COLUMNS of one row; v_permlane16_swap pairs two column blocks into 8
+//     consecutive columns, and the epilogue runs straight from registers (epi_row8: bias, act,
+//     dropout, residual, 16-B stores) -- no LDS stage, no barrier, so the next tile's main loop
+//     starts while the stores drain and each wave group's epilogue overlaps the other's MFMAs;
+//   * tiles are dealt per XCD: the raster (groups of MIT_G256_GROUP row-blocks walking N) is cut
+//     into 8 contiguous chunks, chunk x goes to the workgroups with blockIdx % 8 == x (dispatch
+//     round-robins blocks over XCDs; placement only matters for L2 reuse, never for correctness).
+// ------------------------------------------------------------------------------------------------
+template <int LAY>
+struct DmaLanes {
+  uint32_t off[2][2];  // [half][instr] lane part of the source byte offset (tile origin excluded)
+  int lim[2];          // [instr] lane's row (K-contig) / first column (MN-contig) inside a half
+  uint32_t step;       // bytes per K-tile
+  __device__ __forceinline__ void init(long ld, int w, int lane) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int id = (w * 2 + j) * 64 + lane;
+      if (LAY == MIT_K_CONTIG) {
+        const int r = id >> 3, c = (id & 7) ^ ((r >> 1) & 7);
+        lim[j] = r;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) off[h][j] = (uint32_t)(((h * 128 + r) * ld + c * 8) * 2);
+      } else {
+        const int kr = id >> 4, c = (id & 15) ^ (mn_swz(kr) >> 4);
+        lim[j] = c * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) off[h][j] = (uint32_t)((kr * ld + h * 128 + c * 8) * 2);
+      }
+    }
+    step = LAY == MIT_K_CONTIG ? (uint32_t)(BK * 2) : (uint32_t)(BK * ld * 2);
+  }
+  // origin = byte offset of the tile's first row (K-contig) / column (MN-contig); left = rows /
+  // columns of the operand from there on (the rest reads as zeros)
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* dst, int h, int kt, uint32_t origin,
+                                        int left) const {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t boff = (h * 128 + lim[j] < left) ? off[h][j] + origin + (uint32_t)kt * step : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
+                                               boff, 0, 0, 0);
+    }
+  }
+};
+
+__device__ __forceinline__ void tile_origin(int r, int nbm, int nbn, int& m0, int& n0) {
+  const int GROUP = MIT_G256_GROUP;
+  const int group_id = r / (GROUP * nbn);
+  const int first_m = group_id * GROUP;
+  const int gsize = min(nbm - first_m, GROUP);
+  m0 = (first_m + (r % (GROUP * nbn)) % gsize) * B2;
+  n0 = ((r % (GROUP * nbn)) / gsize) * B2;
+}
+
+// all arguments in one struct, Epi first: the epilogue re-reads Epi / C / ldc / M / N through the
+// kernarg segment pointer (scalar loads, laundered per tile so they are not hoisted), which keeps
+// them out of the SGPRs the main loop needs (the one-tile kernel already sits at the SGPR limit).
+// Host guarantees every element offset fits in 31 bits (32-bit index math).
+struct G256P {
+  Epi e;
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  int M, N, K, lda, ldb, ldc, a_bytes, b_bytes;
+};
+typedef __attribute__((address_space(4))) const G256P* G256PK;
+
+template <int ALAY, int BLAY, int ACT, bool DROP>
+__global__ __launch_bounds__(512) void gemm256p_kernel(G256P p) {
+  static_assert(ALAY == MIT_K_CONTIG, "persistent 256 kernel: K-contig A only");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  const int M = p.M, N = p.N;
+  const int nbn = (N + B2 - 1) / B2, nbm = (M + B2 - 1) / B2;
+  const int ntiles = nbn * nbm;
+  // this workgroup's tiles: r, r + G8, ... < ce (chunk of XCD slot x)
+  const int G8 = (int)(gridDim.x >> 3), x = (int)(blockIdx.x & 7), y = (int)(blockIdx.x >> 3);
+  const int ce = (x + 1) * ntiles >> 3;
+  int r = (x * ntiles >> 3) + y;
+  if (r >= ce) return;  // whole workgroup, before any barrier
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
+  const int nk = p.K / BK;  // even (host guarantees K % 128 == 0)
+  const int lda = p.lda, ldb = p.ldb;
+
+  DmaLanes<ALAY> pa;
+  DmaLanes<BLAY> pb;
+  pa.init(lda, wid, lane);
+  pb.init(ldb, wid, lane);
+
+  // per-tile scalars: byte origin of the tile's A rows / B rows (or columns) and how many remain
+  int m0, n0, m1 = 0, n1 = 0;
+  tile_origin(r, nbm, nbn, m0, n0);
+  bool has_next = r + G8 < ce;
+  if (has_next) tile_origin(r + G8, nbm, nbn, m1, n1);
+  auto a_org = [&](int m) { return (uint32_t)m * (uint32_t)lda * 2u; };
+  auto b_org = [&](int n) { return BLAY == MIT_K_CONTIG ? (uint32_t)n * (uint32_t)ldb * 2u : (uint32_t)n * 2u; };
+  uint32_t ao = a_org(m0), bo = b_org(n0), ao1 = a_org(m1), bo1 = b_org(n1);
+
+  // half-tile LDS-DMA into buffer (t & 1): K-tile t of this tile / K-tile kt of the next tile
+  // (same buffer parity as stream position nk + kt: nk is even)
+  auto issue_cur = [&](int X, int h, int t) {
+    char* dst = smem + (t & 1) * BUF_BYTES + (X * 2 + h) * HALF_BYTES + wid * 2048;
+    if (X == 0) pa.issue(ra, dst, h, t, ao, M - m0);
+    else pb.issue(rb, dst, h, t, bo, N - n0);
+  };
+  auto issue_nxt = [&](int X, int h, int kt) -> bool {
+    if (!has_next) return false;
+    char* dst = smem + (kt & 1) * BUF_BYTES + (X * 2 + h) * HALF_BYTES + wid * 2048;
+    if (X == 0) pa.issue(ra, dst, h, kt, ao1, M - m1);
+    else pb.issue(rb, dst, h, kt, bo1, N - n1);
+    return true;
+  };
+  auto wait_dma = [&](bool younger_issued) {
+    if (younger_issued) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x4 acc[8][4];
+  bf16x8 af[4][2], blo[2][2], bhi[2][2];
+  auto read_a = [&](int buf, int ih) {
+    const char* base = smem + buf * BUF_BYTES + wr * HALF_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag<ALAY>(base, ih * 64 + i * 16, kk, lane);
+  };
+  auto read_b = [&](int buf, int jh, bf16x8 (&bf)[2][2]) {
+    const char* base = smem + buf * BUF_BYTES + (2 + (wc >> 1)) * HALF_BYTES;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = frag<BLAY>(base, (wc & 1) * 64 + jh * 32 + j * 16, kk, lane);
+  };
+  // C^T blocks: lane l holds row (l & 15), columns 4 * (l >> 4) + 0..3 of each 16x16 block
+  auto mma = [&](int ih, int jh, bf16x8 (&bf)[2][2]) {
+    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#if MIT_G256P_SWAP
+          acc[ih * 4 + i][jh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+#else  // timing experiment only: C blocks instead of C^T (the register epilogue then stores a transposed image)
+          acc[ih * 4 + i][jh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+#endif
+    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  // register epilogue: v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane group g with 8
+  // consecutive columns: block 2jp + (g & 1), columns 8 * (g >> 1) .. +8. Gathered (see
+  // epi_gatherable): bias and the 16 residual / aux segments are loaded before the first store.
+  auto epilogue = [&]() {
+    G256PK kp = (G256PK)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));  // re-read per tile, not hoisted into the main loop's SGPRs
+    Epi e;
+    e.bias = kp->e.bias;
+    e.res = kp->e.res;
+    e.ldr = kp->e.ldr;
+    e.aux = kp->e.aux;
+    e.ld_aux = kp->e.ld_aux;
+    e.aux_scale = kp->e.aux_scale;
+    e.alpha = kp->e.alpha;
+    e.act = kp->e.act;
+    e.out_f32 = kp->e.out_f32;
+    e.accumulate = kp->e.accumulate;
+    e.seed = kp->e.seed;
+    e.site = kp->e.site;
+    e.thresh = kp->e.thresh;
+    e.dscale = kp->e.dscale;
+    e.dropout = kp->e.dropout;
+    e.vec = kp->e.vec;
+    void* C = kp->C;
+    const long ldc = kp->ldc, Mk = kp->M, Nk = kp->N;
+    const int g = lane >> 4;
+    const long r0 = m0 + wr * 128 + (lane & 15);
+    const long c0 = n0 + wc * 64 + (g & 1) * 16 + (g >> 1) * 8;
+    auto seg = [&](int i, int jp, float* v) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][t]),
+                                                         __float_as_uint(acc[i][2 * jp + 1][t]), false, false);
+        v[t] = __uint_as_float(sw[0]);
+        v[4 + t] = __uint_as_float(sw[1]);
+      }
+    };
+    if (epi_gatherable(e)) {
+      float b0[8], b1[8];
+      epi_bias8(e, c0, Nk, b0);
+      epi_bias8(e, c0 + 32, Nk, b1);
+      bf16x8 xs[8][2];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) xs[i][jp] = epi_x8(e, Mk, Nk, r0 + i * 16, c0 + jp * 32);
+      const uint64_t key = epi_key<DROP>(e);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          float v[8];
+          seg(i, jp, v);
+          const long gr = r0 + i * 16, gc = c0 + jp * 32;
+          if (gr < Mk && gc < Nk) epi8x<ACT, DROP>(e, C, ldc, Nk, gr, gc, v, jp ? b1 : b0, xs[i][jp], key);
+        }
+    } else {
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          float v[8];
+          seg(i, jp, v);
+          const long gr = r0 + i * 16, gc = c0 + jp * 32;
+          if (gr < Mk && gc < Nk) epi_row8<ACT, DROP>(e, C, ldc, Nk, gr, gc, v);
+        }
+    }
+  };
+
+  // two K-tiles (t in buffer 0, t+1 in buffer 1) in 4 phases, DMA schedule as in gemm256_kernel;
+  // LAST: the DMA slots for t+2 / t+3 carry the next tile's K-tiles 0 / 1 (if any)
+  auto iter = [&](int t, auto last_c) {
+    constexpr bool LAST = decltype(last_c)::value;
+    read_a(0, 0);
+    read_b(0, 0, blo);
+    issue_cur(1, 1, t + 1);
+    read_b(0, 1, bhi);
+    issue_cur(0, 0, t + 1);
+    issue_cur(0, 1, t + 1);
+    bar_raw();
+    mma(0, 0, blo);
+    mma(0, 1, bhi);
+    bar_raw();
+
+    read_a(0, 1);
+    if (LAST) {
+      wait_dma(issue_nxt(1, 0, 0));
+    } else {
+      issue_cur(1, 0, t + 2);
+      wait_dma(true);
+    }
+    bar_raw();
+    mma(1, 1, bhi);
+    mma(1, 0, blo);
+    bar_raw();
+
+    read_a(1, 0);
+    read_b(1, 0, blo);
+    if (LAST) issue_nxt(1, 1, 0);
+    else issue_cur(1, 1, t + 2);
+    read_b(1, 1, bhi);
+    if (LAST) {
+      issue_nxt(0, 0, 0);
+      issue_nxt(0, 1, 0);
+    } else {
+      issue_cur(0, 0, t + 2);
+      issue_cur(0, 1, t + 2);
+    }
+    bar_raw();
+    mma(0, 0, blo);
+    mma(0, 1, bhi);
+    bar_raw();
+
+    read_a(1, 1);
+    if (LAST) {
+      wait_dma(issue_nxt(1, 0, 1));
+    } else {
+      issue_cur(1, 0, t + 3);
+      wait_dma(true);
+    }
+    bar_raw();
+    mma(1, 1, bhi);
+    mma(1, 0, blo);
+    bar_raw();
+  };
+
+  // prologue (first tile only): K-tile 0 (all four halves) and B0 of K-tile 1
+  issue_cur(0, 0, 0);
+  issue_cur(0, 1, 0);
+  issue_cur(1, 0, 0);
+  issue_cur(1, 1, 0);
+  issue_cur(1, 0, 1);
+  wait_dma(true);
+  bar_raw();
+  if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
+
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < nk - 2; t += 2) iter(t, std::false_type{});
+    iter(nk - 2, std::true_type{});
+    // the next tile's K-tile 0 and B0 of its K-tile 1 are in flight / landed; this wave's
+    // epilogue runs in the slot of the next tile's first fragment reads
+#if MIT_G256_NOEPI  // timing experiment only: no output
+    if (acc[0][0][0] == 1234.5f && acc[7][3][3] == 1234.5f) epilogue();
+#else
+    epilogue();
+#endif
+    if (!has_next) break;
+    r += G8;
+    m0 = m1;
+    n0 = n1;
+    ao = ao1;
+    bo = bo1;
+    has_next = r + G8 < ce;
+    if (has_next) {
+      tile_origin(r + G8, nbm, nbn, m1, n1);
+      ao1 = a_org(m1);
+      bo1 = b_org(n1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wr == 0) bar_raw();  // equal barrier counts for both groups at exit
 }
 
 // C = alpha * sum_s slab[s] (f32 or bf16 out, optional accumulate); rowsum = sum_s rowslab[s]
@@ -953,9 +1406,57 @@ void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes,
                      b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
 }
 
+// persistent 256 kernel (gemm256p_kernel) where it applies: 1 = on (default), 0 = the one-tile-per-
+// workgroup kernel (A/B, MIT_G256P=0)
+int g_persist = -1;
+int persist_mode() {
+  if (g_persist < 0) g_persist = getenv("MIT_G256P") ? atoi(getenv("MIT_G256P")) : 0;
+  return g_persist;
+}
+int g_num_cus = 0;
+int num_cus() {
+  if (!g_num_cus) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    g_num_cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount : 256;
+    if (g_num_cus < 8) g_num_cus = 8;
+  }
+  return g_num_cus;
+}
+
 template <int AL, int BL, int ACT, bool DROP>
 void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
   const long nbm = (g->M + B2 - 1) / B2, nbn = (g->N + B2 - 1) / B2;
+  if constexpr (AL == MIT_K_CONTIG) {
+    const long lim = 1L << 31;
+    if (persist_mode() && g->K % (2 * BK) == 0 && g->M * g->ldc < lim && g->N * g->ldc < lim &&
+        (!g->residual || g->M * g->ldr < lim) && (!g->aux || g->M * g->ld_aux < lim) && g->M < lim && g->N < lim &&
+        g->lda < lim && g->ldb < lim) {
+      static bool pattr = false;
+      if (!pattr) {
+        set_lds(gemm256p_kernel<AL, BL, ACT, DROP>, 2 * BUF_BYTES);
+        pattr = true;
+      }
+      // one workgroup per CU at most, a multiple of 8 (the per-XCD tile deal)
+      const long cus = num_cus() & ~7L, nt = nbm * nbn;
+      const long grid = std::min(cus, (nt + 7) & ~7L);
+      G256P p;
+      p.e = e;
+      p.A = (const bf16*)g->A;
+      p.B = (const bf16*)g->B;
+      p.C = g->C;
+      p.M = (int)g->M;
+      p.N = (int)g->N;
+      p.K = (int)g->K;
+      p.lda = (int)g->lda;
+      p.ldb = (int)g->ldb;
+      p.ldc = (int)g->ldc;
+      p.a_bytes = a_bytes;
+      p.b_bytes = b_bytes;
+      hipLaunchKernelGGL((gemm256p_kernel<AL, BL, ACT, DROP>), dim3((unsigned)grid), dim3(512), 2 * BUF_BYTES, s, p);
+      return;
+    }
+  }
   static bool attr = false;
   if (!attr) {
     set_lds(gemm256_kernel<AL, BL, ACT, DROP>, SMEM2_BYTES);
@@ -1079,6 +1580,12 @@ Split plan_split(const mit_gemm_args* g) {
 extern "C" int mit_gemm_set_variant(int v) {
   MIT_CHECK_ARG(v >= 0 && v <= 2, "mit_gemm_set_variant: %d not in {0,1,2}", v);
   g_variant = v;
+  return MIT_OK;
+}
+
+extern "C" int mit_gemm_set_persistent(int on) {
+  MIT_CHECK_ARG(on == 0 || on == 1, "mit_gemm_set_persistent: %d not in {0,1}", on);
+  g_persist = on;
   return MIT_OK;
 }
 
