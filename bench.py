@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
-PMC_SUMMARY = "r01_bench_pmc.json"
+PMC_SUMMARY = "r02_pmc.json"
 METRIC = "image-caption pairs/sec (train step), 6L/d512 decoder + ViT-B/16, 1/2/4/8 GPU"
 
 
@@ -78,7 +78,7 @@ class GemmProbe:
     in their original order, back-to-back, `passes` times, between ONE event pair per kernel
     instance (tile kernel, a_layout, b_layout; native.gemm_plan) -- this is the per-launch kernel duration (event markers between
     kernels add a dispatch ramp that the kernel itself does not spend; rocprofv3's per-dispatch
-    average, profiles/r01_bench_kernel_stats.csv, is the cross-check)."""
+    average, profiles/r02_bench_kernel_stats.csv, is the cross-check)."""
 
     def __init__(self):
         self.rec = []
@@ -154,7 +154,7 @@ class GemmProbe:
 def pmc_traffic(kernel_prefix):
     """HBM bytes per launch of a kernel (averaged over the launches of all its template instances)
     from the committed rocprofv3 PMC summary (FETCH_SIZE and
-    WRITE_SIZE passes of tools/profile_r01.sh over this same command, condensed by
+    WRITE_SIZE passes of tools/profile_r02.sh over this same command, condensed by
     tools/rocpd_summary.py); None when no summary is present."""
     path = os.path.join(ROOT, "profiles", PMC_SUMMARY)
     try:

@@ -114,11 +114,6 @@ int mit_gemm_set_variant(int variant);
 /* In-launch split-K combine (see workspace above): 0 = off (default; env MIT_GEMM_FUSED_SPLIT=1
  * seeds it on), 1 = on. A scheduling knob: results equal up to fp32 summation order. */
 int mit_gemm_set_fused_split(int on);
-/* Persistent form of the 256x256 kernel (K-contig A, K a multiple of 128): one workgroup per CU
- * walks its tiles with the K-tile DMA stream running across tile boundaries and a register
- * epilogue. 1 = on (default; env MIT_G256P=0 seeds it off), 0 = one tile per workgroup. A
- * scheduling knob: results equal up to fp32 summation order (identical summation order in fact). */
-int mit_gemm_set_persistent(int on);
 /* The launch mit_gemm would make for these args (no launch): returns the output tile edge of the
  * kernel (256 or 128 for bf16, 64 for the f32 kernel, 0 for an empty problem) and stores the
  * split-K factor in *ksplit (may be NULL). For profiling tools that attribute kernel time. */

@@ -18,16 +18,19 @@
 //     tiles are read with ds_read_b64_tr_b16 (CDNA4 hardware transpose) so one kernel serves
 //     NT / NN / TN without materialising a transpose. Out-of-range chunks get a buffer offset
 //     past num_records and read as zeros: no edge branches in the main loops.
-//   * epilogue: accumulators staged through LDS, then each lane applies the fused epilogue to 8
-//     consecutive columns and writes 16 bytes. The activation and dropout are TEMPLATE
-//     parameters (an 8-wide GELU / dropout-hash epilogue evaluated behind runtime flags costs
-//     ~20 % of a K=768 GEMM); bias / residual / aux-mask / f32-accumulate stay runtime flags.
+//   * epilogue: each lane applies the fused epilogue to 8 consecutive columns and writes 16 bytes,
+//     with every operand load (bias, residual / aux mask) issued before the tile's first store
+//     (vmcnt counts stores on gfx9). The 128 kernel stages accumulators through LDS; the 256
+//     kernel (K-contig A) accumulates C^T blocks (swapped MFMA operands) so a lane holds 4
+//     consecutive columns, and v_permlane16_swap pairs make 8 -- no LDS stage, no barrier. The
+//     activation and dropout are TEMPLATE parameters (an 8-wide GELU / dropout-hash epilogue
+//     evaluated behind runtime flags costs ~20 % of a K=768 GEMM); bias / residual / aux-mask /
+//     f32-accumulate stay runtime flags.
 //   * tile order: XCD-aware remap + row grouping so tiles sharing A/B panels share an L2.
 // fp32 path (parity mode): a plain LDS-tiled FMA kernel with the identical epilogue semantics.
 #include <stdlib.h>
 
 #include <cmath>
-#include <type_traits>
 
 #include "common.h"
 
@@ -610,11 +613,8 @@ __device__ __forceinline__ void bar_raw() {
 #ifndef MIT_G256_EARLY_A1
 #define MIT_G256_EARLY_A1 1
 #endif
-#ifndef MIT_G256_NOEPI
-#define MIT_G256_NOEPI 0
-#endif
-#ifndef MIT_G256P_SWAP
-#define MIT_G256P_SWAP 1
+#ifndef MIT_G256_REGEPI  // register epilogue in the one-tile 256 kernel (K-contig A)
+#define MIT_G256_REGEPI 1
 #endif
 #ifndef MIT_G256_PRIO  // raise the wave priority around each MFMA block
 #define MIT_G256_PRIO 1
@@ -658,6 +658,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
 
   constexpr bool TN = ALAY == MIT_MN_CONTIG && BLAY == MIT_MN_CONTIG;
   const bool do_rs = TN && rowsum != nullptr && bn == 0 && wc == 0;
+  // REG: accumulate C^T blocks (MFMA operands swapped: a lane holds 4 consecutive columns of one
+  // row) so the epilogue can run from registers (no LDS stage, no barrier); used when the epilogue
+  // is gatherable, else the C^T blocks are staged through LDS transposed
+  constexpr bool REG = ALAY == MIT_K_CONTIG && MIT_G256_REGEPI;
+  const bool regepi = REG && ksplit == 1 && epi_gatherable(e);
   float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   const int nk = (int)((ke - kb + BK - 1) / BK);
@@ -709,7 +714,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[ih * 4 + i][jh * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+              REG ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0)
+                  : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
     if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
@@ -778,7 +784,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       mma(1, 1, bhi);
       mma(1, 0, blo);
     }
-    bar_raw();
+    // register epilogue: the lagging group skips the loop's last barrier (nothing after it reads
+    // LDS), so the leading group's epilogue overlaps its last MFMA block and neither waits
+    if (!(regepi && wr == 1 && t + 2 >= nk)) bar_raw();
   }
 #else
   for (int t = 0; t < nk; t += 2) {
@@ -837,6 +845,38 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   }
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (regepi) {
+    // gathered register epilogue: v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane
+    // group g with 8 consecutive columns: block 2jp + (g & 1), columns 8 * (g >> 1) .. +8
+    const int g = lane >> 4;
+    const long r0 = m0 + wr * 128 + (lane & 15);
+    const long c0 = n0 + wc * 64 + (g & 1) * 16 + (g >> 1) * 8;
+    float b0[8], b1[8];
+    epi_bias8(e, c0, N, b0);
+    epi_bias8(e, c0 + 32, N, b1);
+    bf16x8 xs[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) xs[i][jp] = epi_x8(e, M, N, r0 + i * 16, c0 + jp * 32);
+    const uint64_t key = epi_key<DROP>(e);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][t]),
+                                                           __float_as_uint(acc[i][2 * jp + 1][t]), false, false);
+          v[t] = __uint_as_float(sw[0]);
+          v[4 + t] = __uint_as_float(sw[1]);
+        }
+        const long gr = r0 + i * 16, gc = c0 + jp * 32;
+        if (gr < M && gc < N) epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v, jp ? b1 : b0, xs[i][jp], key);
+      }
+    return;
+  }
   if (wr == 0) bar_raw();  // re-align the groups
   bar_raw();
 
@@ -853,9 +893,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   }
 
   // ---- epilogue: per wave, two passes of 64 rows x 64 cols through a private fp32 LDS stage ----
-#if MIT_G256_NOEPI  // timing experiment only: no output
-  if (acc[0][0][0] != 1234.5f || acc[7][3][3] != 1234.5f) return;
-#endif
   float* cs = (float*)smem + wid * 64 * EPI_LD;
   const bool gather = ksplit == 1 && epi_gatherable(e);
   const long gcw = n0 + wc * 64 + (lane & 7) * 8;  // this lane's columns in every pass / row
@@ -873,7 +910,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-          cs[(i * 16 + (lane >> 4) * 4 + t) * EPI_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][t];
+          if (REG)  // C^T block: lane holds row (lane & 15), columns 4 * (lane >> 4) + t
+            cs[(i * 16 + (lane & 15)) * EPI_LD + j * 16 + (lane >> 4) * 4 + t] = acc[pass * 4 + i][j][t];
+          else
+            cs[(i * 16 + (lane >> 4) * 4 + t) * EPI_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][t];
     __builtin_amdgcn_wave_barrier();
     if (gather) {  // this pass's residual / aux segments first, then only stores
       bf16x8 xs[8];
@@ -909,334 +949,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     }
     __builtin_amdgcn_wave_barrier();
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Persistent 256x256 kernel (NT / NN with K-contig A, K a multiple of 128). Same tile, waves, LDS
-// images, DMA schedule and 4-barrier-per-K-tile ping-pong as gemm256_kernel, with three changes
-// aimed at the per-tile fixed cost that dominates the encoder's K = 768 shapes (one launch round of
-// the 256 kernel = ~9 us of prologue fill + LDS-staged epilogue + store burst, i.e. 7 K-steps):
-//   * one workgroup per CU walks a list of tiles; the K-tile stream runs on ACROSS tiles, so the
-//     last K-tiles of tile n already DMA tile n+1's first K-tiles (no prologue after the first);
-//   * the MFMA operands are swapped (acc = B-frag x A-frag, i.e. C^T per 16x16 block), so a lane
-//     holds 4 consecutive COLUMNS of one row; v_permlane16_swap pairs two column blocks into 8
-//     consecutive columns, and the epilogue runs straight from registers (epi_row8: bias, act,
-//     dropout, residual, 16-B stores) -- no LDS stage, no barrier, so the next tile's main loop
-//     starts while the stores drain and each wave group's epilogue overlaps the other's MFMAs;
-//   * tiles are dealt per XCD: the raster (groups of MIT_G256_GROUP row-blocks walking N) is cut
-//     into 8 contiguous chunks, chunk x goes to the workgroups with blockIdx % 8 == x (dispatch
-//     round-robins blocks over XCDs; placement only matters for L2 reuse, never for correctness).
-// ------------------------------------------------------------------------------------------------
-template <int LAY>
-struct DmaLanes {
-  uint32_t off[2][2];  // [half][instr] lane part of the source byte offset (tile origin excluded)
-  int lim[2];          // [instr] lane's row (K-contig) / first column (MN-contig) inside a half
-  uint32_t step;       // bytes per K-tile
-  __device__ __forceinline__ void init(long ld, int w, int lane) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int id = (w * 2 + j) * 64 + lane;
-      if (LAY == MIT_K_CONTIG) {
-        const int r = id >> 3, c = (id & 7) ^ ((r >> 1) & 7);
-        lim[j] = r;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) off[h][j] = (uint32_t)(((h * 128 + r) * ld + c * 8) * 2);
-      } else {
-        const int kr = id >> 4, c = (id & 15) ^ (mn_swz(kr) >> 4);
-        lim[j] = c * 8;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) off[h][j] = (uint32_t)((kr * ld + h * 128 + c * 8) * 2);
-      }
-    }
-    step = LAY == MIT_K_CONTIG ? (uint32_t)(BK * 2) : (uint32_t)(BK * ld * 2);
-  }
-  // origin = byte offset of the tile's first row (K-contig) / column (MN-contig); left = rows /
-  // columns of the operand from there on (the rest reads as zeros)
-  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* dst, int h, int kt, uint32_t origin,
-                                        int left) const {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const uint32_t boff = (h * 128 + lim[j] < left) ? off[h][j] + origin + (uint32_t)kt * step : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16,
-                                               boff, 0, 0, 0);
-    }
-  }
-};
-
-__device__ __forceinline__ void tile_origin(int r, int nbm, int nbn, int& m0, int& n0) {
-  const int GROUP = MIT_G256_GROUP;
-  const int group_id = r / (GROUP * nbn);
-  const int first_m = group_id * GROUP;
-  const int gsize = min(nbm - first_m, GROUP);
-  m0 = (first_m + (r % (GROUP * nbn)) % gsize) * B2;
-  n0 = ((r % (GROUP * nbn)) / gsize) * B2;
-}
-
-// all arguments in one struct, Epi first: the epilogue re-reads Epi / C / ldc / M / N through the
-// kernarg segment pointer (scalar loads, laundered per tile so they are not hoisted), which keeps
-// them out of the SGPRs the main loop needs (the one-tile kernel already sits at the SGPR limit).
-// Host guarantees every element offset fits in 31 bits (32-bit index math).
-struct G256P {
-  Epi e;
-  const bf16* A;
-  const bf16* B;
-  void* C;
-  int M, N, K, lda, ldb, ldc, a_bytes, b_bytes;
-};
-typedef __attribute__((address_space(4))) const G256P* G256PK;
-
-template <int ALAY, int BLAY, int ACT, bool DROP>
-__global__ __launch_bounds__(512) void gemm256p_kernel(G256P p) {
-  static_assert(ALAY == MIT_K_CONTIG, "persistent 256 kernel: K-contig A only");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-
-  const int M = p.M, N = p.N;
-  const int nbn = (N + B2 - 1) / B2, nbm = (M + B2 - 1) / B2;
-  const int ntiles = nbn * nbm;
-  // this workgroup's tiles: r, r + G8, ... < ce (chunk of XCD slot x)
-  const int G8 = (int)(gridDim.x >> 3), x = (int)(blockIdx.x & 7), y = (int)(blockIdx.x >> 3);
-  const int ce = (x + 1) * ntiles >> 3;
-  int r = (x * ntiles >> 3) + y;
-  if (r >= ce) return;  // whole workgroup, before any barrier
-
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.b_bytes, 0x00020000);
-  const int nk = p.K / BK;  // even (host guarantees K % 128 == 0)
-  const int lda = p.lda, ldb = p.ldb;
-
-  DmaLanes<ALAY> pa;
-  DmaLanes<BLAY> pb;
-  pa.init(lda, wid, lane);
-  pb.init(ldb, wid, lane);
-
-  // per-tile scalars: byte origin of the tile's A rows / B rows (or columns) and how many remain
-  int m0, n0, m1 = 0, n1 = 0;
-  tile_origin(r, nbm, nbn, m0, n0);
-  bool has_next = r + G8 < ce;
-  if (has_next) tile_origin(r + G8, nbm, nbn, m1, n1);
-  auto a_org = [&](int m) { return (uint32_t)m * (uint32_t)lda * 2u; };
-  auto b_org = [&](int n) { return BLAY == MIT_K_CONTIG ? (uint32_t)n * (uint32_t)ldb * 2u : (uint32_t)n * 2u; };
-  uint32_t ao = a_org(m0), bo = b_org(n0), ao1 = a_org(m1), bo1 = b_org(n1);
-
-  // half-tile LDS-DMA into buffer (t & 1): K-tile t of this tile / K-tile kt of the next tile
-  // (same buffer parity as stream position nk + kt: nk is even)
-  auto issue_cur = [&](int X, int h, int t) {
-    char* dst = smem + (t & 1) * BUF_BYTES + (X * 2 + h) * HALF_BYTES + wid * 2048;
-    if (X == 0) pa.issue(ra, dst, h, t, ao, M - m0);
-    else pb.issue(rb, dst, h, t, bo, N - n0);
-  };
-  auto issue_nxt = [&](int X, int h, int kt) -> bool {
-    if (!has_next) return false;
-    char* dst = smem + (kt & 1) * BUF_BYTES + (X * 2 + h) * HALF_BYTES + wid * 2048;
-    if (X == 0) pa.issue(ra, dst, h, kt, ao1, M - m1);
-    else pb.issue(rb, dst, h, kt, bo1, N - n1);
-    return true;
-  };
-  auto wait_dma = [&](bool younger_issued) {
-    if (younger_issued) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
-  f32x4 acc[8][4];
-  bf16x8 af[4][2], blo[2][2], bhi[2][2];
-  auto read_a = [&](int buf, int ih) {
-    const char* base = smem + buf * BUF_BYTES + wr * HALF_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag<ALAY>(base, ih * 64 + i * 16, kk, lane);
-  };
-  auto read_b = [&](int buf, int jh, bf16x8 (&bf)[2][2]) {
-    const char* base = smem + buf * BUF_BYTES + (2 + (wc >> 1)) * HALF_BYTES;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = frag<BLAY>(base, (wc & 1) * 64 + jh * 32 + j * 16, kk, lane);
-  };
-  // C^T blocks: lane l holds row (l & 15), columns 4 * (l >> 4) + 0..3 of each 16x16 block
-  auto mma = [&](int ih, int jh, bf16x8 (&bf)[2][2]) {
-    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#if MIT_G256P_SWAP
-          acc[ih * 4 + i][jh * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
-#else  // timing experiment only: C blocks instead of C^T (the register epilogue then stores a transposed image)
-          acc[ih * 4 + i][jh * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
-#endif
-    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(0);
-  };
-  // register epilogue: v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane group g with 8
-  // consecutive columns: block 2jp + (g & 1), columns 8 * (g >> 1) .. +8. Gathered (see
-  // epi_gatherable): bias and the 16 residual / aux segments are loaded before the first store.
-  auto epilogue = [&]() {
-    G256PK kp = (G256PK)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(kp));  // re-read per tile, not hoisted into the main loop's SGPRs
-    Epi e;
-    e.bias = kp->e.bias;
-    e.res = kp->e.res;
-    e.ldr = kp->e.ldr;
-    e.aux = kp->e.aux;
-    e.ld_aux = kp->e.ld_aux;
-    e.aux_scale = kp->e.aux_scale;
-    e.alpha = kp->e.alpha;
-    e.act = kp->e.act;
-    e.out_f32 = kp->e.out_f32;
-    e.accumulate = kp->e.accumulate;
-    e.seed = kp->e.seed;
-    e.site = kp->e.site;
-    e.thresh = kp->e.thresh;
-    e.dscale = kp->e.dscale;
-    e.dropout = kp->e.dropout;
-    e.vec = kp->e.vec;
-    void* C = kp->C;
-    const long ldc = kp->ldc, Mk = kp->M, Nk = kp->N;
-    const int g = lane >> 4;
-    const long r0 = m0 + wr * 128 + (lane & 15);
-    const long c0 = n0 + wc * 64 + (g & 1) * 16 + (g >> 1) * 8;
-    auto seg = [&](int i, int jp, float* v) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][t]),
-                                                         __float_as_uint(acc[i][2 * jp + 1][t]), false, false);
-        v[t] = __uint_as_float(sw[0]);
-        v[4 + t] = __uint_as_float(sw[1]);
-      }
-    };
-    if (epi_gatherable(e)) {
-      float b0[8], b1[8];
-      epi_bias8(e, c0, Nk, b0);
-      epi_bias8(e, c0 + 32, Nk, b1);
-      bf16x8 xs[8][2];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) xs[i][jp] = epi_x8(e, Mk, Nk, r0 + i * 16, c0 + jp * 32);
-      const uint64_t key = epi_key<DROP>(e);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          float v[8];
-          seg(i, jp, v);
-          const long gr = r0 + i * 16, gc = c0 + jp * 32;
-          if (gr < Mk && gc < Nk) epi8x<ACT, DROP>(e, C, ldc, Nk, gr, gc, v, jp ? b1 : b0, xs[i][jp], key);
-        }
-    } else {
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          float v[8];
-          seg(i, jp, v);
-          const long gr = r0 + i * 16, gc = c0 + jp * 32;
-          if (gr < Mk && gc < Nk) epi_row8<ACT, DROP>(e, C, ldc, Nk, gr, gc, v);
-        }
-    }
-  };
-
-  // two K-tiles (t in buffer 0, t+1 in buffer 1) in 4 phases, DMA schedule as in gemm256_kernel;
-  // LAST: the DMA slots for t+2 / t+3 carry the next tile's K-tiles 0 / 1 (if any)
-  auto iter = [&](int t, auto last_c) {
-    constexpr bool LAST = decltype(last_c)::value;
-    read_a(0, 0);
-    read_b(0, 0, blo);
-    issue_cur(1, 1, t + 1);
-    read_b(0, 1, bhi);
-    issue_cur(0, 0, t + 1);
-    issue_cur(0, 1, t + 1);
-    bar_raw();
-    mma(0, 0, blo);
-    mma(0, 1, bhi);
-    bar_raw();
-
-    read_a(0, 1);
-    if (LAST) {
-      wait_dma(issue_nxt(1, 0, 0));
-    } else {
-      issue_cur(1, 0, t + 2);
-      wait_dma(true);
-    }
-    bar_raw();
-    mma(1, 1, bhi);
-    mma(1, 0, blo);
-    bar_raw();
-
-    read_a(1, 0);
-    read_b(1, 0, blo);
-    if (LAST) issue_nxt(1, 1, 0);
-    else issue_cur(1, 1, t + 2);
-    read_b(1, 1, bhi);
-    if (LAST) {
-      issue_nxt(0, 0, 0);
-      issue_nxt(0, 1, 0);
-    } else {
-      issue_cur(0, 0, t + 2);
-      issue_cur(0, 1, t + 2);
-    }
-    bar_raw();
-    mma(0, 0, blo);
-    mma(0, 1, bhi);
-    bar_raw();
-
-    read_a(1, 1);
-    if (LAST) {
-      wait_dma(issue_nxt(1, 0, 1));
-    } else {
-      issue_cur(1, 0, t + 3);
-      wait_dma(true);
-    }
-    bar_raw();
-    mma(1, 1, bhi);
-    mma(1, 0, blo);
-    bar_raw();
-  };
-
-  // prologue (first tile only): K-tile 0 (all four halves) and B0 of K-tile 1
-  issue_cur(0, 0, 0);
-  issue_cur(0, 1, 0);
-  issue_cur(1, 0, 0);
-  issue_cur(1, 1, 0);
-  issue_cur(1, 0, 1);
-  wait_dma(true);
-  bar_raw();
-  if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
-
-  for (;;) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < nk - 2; t += 2) iter(t, std::false_type{});
-    iter(nk - 2, std::true_type{});
-    // the next tile's K-tile 0 and B0 of its K-tile 1 are in flight / landed; this wave's
-    // epilogue runs in the slot of the next tile's first fragment reads
-#if MIT_G256_NOEPI  // timing experiment only: no output
-    if (acc[0][0][0] == 1234.5f && acc[7][3][3] == 1234.5f) epilogue();
-#else
-    epilogue();
-#endif
-    if (!has_next) break;
-    r += G8;
-    m0 = m1;
-    n0 = n1;
-    ao = ao1;
-    bo = bo1;
-    has_next = r + G8 < ce;
-    if (has_next) {
-      tile_origin(r + G8, nbm, nbn, m1, n1);
-      ao1 = a_org(m1);
-      bo1 = b_org(n1);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (wr == 0) bar_raw();  // equal barrier counts for both groups at exit
 }
 
 // C = alpha * sum_s slab[s] (f32 or bf16 out, optional accumulate); rowsum = sum_s rowslab[s]
@@ -1406,57 +1118,9 @@ void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes,
                      b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
 }
 
-// persistent 256 kernel (gemm256p_kernel) where it applies: 1 = on (default), 0 = the one-tile-per-
-// workgroup kernel (A/B, MIT_G256P=0)
-int g_persist = -1;
-int persist_mode() {
-  if (g_persist < 0) g_persist = getenv("MIT_G256P") ? atoi(getenv("MIT_G256P")) : 0;
-  return g_persist;
-}
-int g_num_cus = 0;
-int num_cus() {
-  if (!g_num_cus) {
-    int dev = 0;
-    hipDeviceProp_t p;
-    g_num_cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount : 256;
-    if (g_num_cus < 8) g_num_cus = 8;
-  }
-  return g_num_cus;
-}
-
 template <int AL, int BL, int ACT, bool DROP>
 void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
   const long nbm = (g->M + B2 - 1) / B2, nbn = (g->N + B2 - 1) / B2;
-  if constexpr (AL == MIT_K_CONTIG) {
-    const long lim = 1L << 31;
-    if (persist_mode() && g->K % (2 * BK) == 0 && g->M * g->ldc < lim && g->N * g->ldc < lim &&
-        (!g->residual || g->M * g->ldr < lim) && (!g->aux || g->M * g->ld_aux < lim) && g->M < lim && g->N < lim &&
-        g->lda < lim && g->ldb < lim) {
-      static bool pattr = false;
-      if (!pattr) {
-        set_lds(gemm256p_kernel<AL, BL, ACT, DROP>, 2 * BUF_BYTES);
-        pattr = true;
-      }
-      // one workgroup per CU at most, a multiple of 8 (the per-XCD tile deal)
-      const long cus = num_cus() & ~7L, nt = nbm * nbn;
-      const long grid = std::min(cus, (nt + 7) & ~7L);
-      G256P p;
-      p.e = e;
-      p.A = (const bf16*)g->A;
-      p.B = (const bf16*)g->B;
-      p.C = g->C;
-      p.M = (int)g->M;
-      p.N = (int)g->N;
-      p.K = (int)g->K;
-      p.lda = (int)g->lda;
-      p.ldb = (int)g->ldb;
-      p.ldc = (int)g->ldc;
-      p.a_bytes = a_bytes;
-      p.b_bytes = b_bytes;
-      hipLaunchKernelGGL((gemm256p_kernel<AL, BL, ACT, DROP>), dim3((unsigned)grid), dim3(512), 2 * BUF_BYTES, s, p);
-      return;
-    }
-  }
   static bool attr = false;
   if (!attr) {
     set_lds(gemm256_kernel<AL, BL, ACT, DROP>, SMEM2_BYTES);
@@ -1580,12 +1244,6 @@ Split plan_split(const mit_gemm_args* g) {
 extern "C" int mit_gemm_set_variant(int v) {
   MIT_CHECK_ARG(v >= 0 && v <= 2, "mit_gemm_set_variant: %d not in {0,1,2}", v);
   g_variant = v;
-  return MIT_OK;
-}
-
-extern "C" int mit_gemm_set_persistent(int on) {
-  MIT_CHECK_ARG(on == 0 || on == 1, "mit_gemm_set_persistent: %d not in {0,1}", on);
-  g_persist = on;
   return MIT_OK;
 }
 

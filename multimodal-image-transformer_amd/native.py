@@ -66,7 +66,6 @@ SIGNATURES = {
     "mit_gemm_set_variant": (I, [I]),
     "mit_gemm_plan": (I, [ctypes.POINTER(GemmArgs), ctypes.POINTER(I)]),
     "mit_gemm_set_fused_split": (I, [I]),
-    "mit_gemm_set_persistent": (I, [I]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
@@ -342,11 +341,6 @@ def gemm_set_variant(v):
 def gemm_set_fused_split(on):
     """In-launch split-K combine for the <= 128-tile GEMMs (off by default)."""
     _check(lib().mit_gemm_set_fused_split(1 if on else 0), "mit_gemm_set_fused_split")
-
-
-def gemm_set_persistent(on):
-    """Persistent 256x256 GEMM (cross-tile K-stream, register epilogue) on / off (on by default)."""
-    _check(lib().mit_gemm_set_persistent(1 if on else 0), "mit_gemm_set_persistent")
 
 
 def gemm_plan(g):

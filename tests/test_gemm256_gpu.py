@@ -22,7 +22,6 @@ def _lib():
     yield
     N.gemm_set_variant(0)
     N.gemm_set_fused_split(0)
-    N.gemm_set_persistent(1)
 
 
 def _ops(M, Nn, K, al, bl, seed=0):
@@ -167,79 +166,3 @@ def test_gemm_split_k_in_launch_combine(al, bl, M, Nn, K, epi):
     scale = max(outs[0].float().abs().max().item(), 1.0)
     assert d <= (2e-2 if out_dt == torch.bfloat16 else 1e-4) * scale, d
 
-
-# persistent 256 kernel (gemm256p_kernel): K-contig A, K % 128 == 0; several tiles per workgroup once
-# the grid exceeds the CU count (12608 x 2304 = 450 tiles), ragged M / N edges, every epilogue
-P_SHAPES = [(256, 256, 128), (264, 136, 256), (1000, 520, 384), (12608, 2304, 768), (4040, 3080, 256), (2056, 768, 3072)]
-
-
-@pytest.mark.parametrize("bl", [0, 1])
-@pytest.mark.parametrize("M,Nn,K", P_SHAPES)
-def test_gemm256_persistent_matches_one_tile_kernel(bl, M, Nn, K):
-    """Same tiles, same per-element summation order (K-tiles in order, 2 MFMA k-slices each): the
-    persistent kernel's output equals the one-tile-per-workgroup kernel's bit for bit."""
-    A, B, ref = _ops(M, Nn, K, 0, bl, seed=M + Nn)
-    N.gemm_set_variant(2)
-    outs = []
-    for pers in (1, 0):
-        N.gemm_set_persistent(pers)
-        C = torch.empty(M, Nn, device=dev(), dtype=torch.float32)
-        N.gemm(A, B, C, M, Nn, K, b_layout=bl)
-        outs.append(C)
-    N.gemm_set_persistent(1)
-    assert _rel(outs[0], ref) < 1e-5
-    assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("M,Nn,K", [(600, 520, 256), (12608, 3072, 768), (1032, 776, 128)])
-def test_gemm256_persistent_epilogues(M, Nn, K):
-    """bias + ReLU / GELU / quick-GELU + residual (bf16 out), alpha + f32 accumulate, ReLU + dropout,
-    and the aux mask: persistent vs the one-tile kernel, bit-identical."""
-    N.gemm_set_variant(2)
-    g = torch.Generator().manual_seed(7)
-    x = torch.randn(M, K, generator=g).to(dev(), torch.bfloat16)
-    w = (torch.randn(Nn, K, generator=g) / 10).to(dev(), torch.bfloat16)
-    bias = torch.randn(Nn, generator=g).to(dev())
-    res = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
-    aux = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
-    seed = torch.tensor([99], dtype=torch.int64, device=dev())
-    acc0 = torch.randn(M, Nn, generator=g).to(dev())
-    base = x.float() @ w.float().t()
-    cases = [dict(bias=bias, act=a, residual=res) for a in (N.ACT_RELU, N.ACT_GELU, N.ACT_QUICK_GELU)]
-    cases += [dict(bias=bias, act=N.ACT_RELU, drop_p=0.1, seed=seed, site=5), dict(aux=aux, aux_scale=1.5), dict()]
-    for kw in cases:
-        outs = []
-        for pers in (1, 0):
-            N.gemm_set_persistent(pers)
-            out = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
-            N.gemm(x, w, out, M, Nn, K, **kw)
-            outs.append(out)
-        assert torch.equal(outs[0], outs[1]), kw
-    outs = []
-    for pers in (1, 0):
-        N.gemm_set_persistent(pers)
-        acc = acc0.clone()
-        N.gemm(x, w, acc, M, Nn, K, alpha=0.5, accumulate=True)
-        outs.append(acc)
-    N.gemm_set_persistent(1)
-    assert torch.equal(outs[0], outs[1])
-    assert _rel(outs[0], acc0 + 0.5 * base) < 1e-5
-
-
-@pytest.mark.parametrize("bl,M,Nn,K", [(0, 12608, 2304, 768), (1, 5000, 1032, 512)])
-def test_gemm256_persistent_race_screen(bl, M, Nn, K):
-    """the cross-tile K-stream (next tile's DMA during this tile's last K-tiles) must be race-free:
-    30 repeats bit-identical"""
-    N.gemm_set_variant(2)
-    N.gemm_set_persistent(1)
-    A, B, ref = _ops(M, Nn, K, 0, bl, seed=4)
-    C0 = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
-    N.gemm(A, B, C0, M, Nn, K, b_layout=bl)
-    assert _rel(C0, ref) < 8e-3
-    C = torch.empty_like(C0)
-    bad = 0
-    for _ in range(30):
-        C.fill_(0)
-        N.gemm(A, B, C, M, Nn, K, b_layout=bl)
-        bad += int(not torch.equal(C, C0))
-    assert bad == 0, f"{bad}/30 repeats differ bitwise"

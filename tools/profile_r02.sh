@@ -1,0 +1,18 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py (run on the GPU box from the repo root; outputs to gpurun_out/):
+#   1) kernel trace + stats of the default bench command (native replay, encoder prefetch stream,
+#      weight-gradient side stream) -> trace   [timeline: tools/timeline.py]
+#   2) the same with --no-prefetch (encoder inline: per-kernel attribution without overlap)
+#   3) FETCH_SIZE and 4) WRITE_SIZE, each in its own pass (TCC slots; MI355X_MICROARCH.md HBM
+#      section) over the default command
+# Condense with tools/rocpd_summary.py into profiles/.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/prof_r02
+mkdir -p $OUT
+ARGS="--no-cpu-baseline --steps 10 --warmup 3"
+P="rocprofv3 --output-format rocpd csv"
+timeout -k 10 300 $P --kernel-trace --stats -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.json 2> $OUT/trace.err &&
+timeout -k 10 300 $P --kernel-trace --stats -d $OUT/trace_noprefetch -o run -- python3 bench.py $ARGS --no-prefetch --no-roofline > $OUT/trace_noprefetch.json 2> $OUT/trace_noprefetch.err &&
+timeout -k 10 300 $P --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run -- python3 bench.py $ARGS --no-roofline > $OUT/fetch.json 2> $OUT/fetch.err &&
+timeout -k 10 300 $P --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o run -- python3 bench.py $ARGS --no-roofline > $OUT/write.json 2> $OUT/write.err

@@ -13,7 +13,11 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     ad = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
-    a, b = ad[-2] + 1, ad[-1] + 1
+    # the shortest span between consecutive AdamW launches with no foreign kernel in it (bench.py's
+    # roofline probe and the timing spin run after the timed steps)
+    spans = [(int(rows[j]["End_Timestamp"]) - int(rows[i + 1]["Start_Timestamp"]), i + 1, j + 1)
+             for i, j in zip(ad, ad[1:]) if not any("spin" in r["Kernel_Name"] for r in rows[i + 1:j + 1])]
+    _, a, b = min(spans)
     step = rows[a:b]
     t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
     ev = []
