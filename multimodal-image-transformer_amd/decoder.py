@@ -487,8 +487,8 @@ class TransformerDecoder:
         def ready(first, last):
             if grads_ready is None:
                 return
-            if side is None:
-                grads_ready(first, last)
+            if side is None:  # a host step of a recorded program (replayed in place)
+                native.host_call(lambda: grads_ready(first, last))
             else:
                 side.under(lambda: grads_ready(first, last))
 
