@@ -99,7 +99,7 @@ class GemmProbe:
         """(kernel template, a_layout, b_layout) of the launch mit_gemm makes for args g."""
         import native
         tile, ks = native.gemm_plan(g)
-        return ("gemm256_kernel" if tile == 256 else "gemm_bf16_kernel", al, bl)
+        return ({256: "gemm256_kernel", 65: "gemm_rs_kernel"}.get(tile, "gemm_bf16_kernel"), al, bl)
 
     def after(self, g):
         import ctypes

@@ -108,14 +108,16 @@ typedef struct {
 int mit_gemm(const mit_gemm_args* args, void* stream);
 long mit_gemm_workspace_bytes(long M, long N, long K);
 /* Tile-kernel choice for bf16 GEMMs: 0 = per shape (default; env MIT_GEMM_VARIANT seeds it),
- * 1 = 128x128 kernel only, 2 = 256x256 kernel wherever split-K is not planned. Results are
+ * 1 = 128x128 kernel only, 2 = 256x256 kernel wherever split-K is not planned, 3 = the 64x64
+ * register-streaming kernel for every NT GEMM without rowsum / split-K. Results are
  * identical up to fp32 summation order; a tuning / test knob, not a numerics switch. */
 int mit_gemm_set_variant(int variant);
 /* In-launch split-K combine (see workspace above): 0 = off (default; env MIT_GEMM_FUSED_SPLIT=1
  * seeds it on), 1 = on. A scheduling knob: results equal up to fp32 summation order. */
 int mit_gemm_set_fused_split(int on);
 /* The launch mit_gemm would make for these args (no launch): returns the output tile edge of the
- * kernel (256 or 128 for bf16, 64 for the f32 kernel, 0 for an empty problem) and stores the
+ * kernel (256 or 128 for bf16, 65 for the bf16 64x64 register-streaming kernel, 64 for the f32
+ * kernel, 0 for an empty problem) and stores the
  * split-K factor in *ksplit (may be NULL). For profiling tools that attribute kernel time. */
 int mit_gemm_plan(const mit_gemm_args* args, int* ksplit);
 

@@ -310,24 +310,35 @@ __device__ __forceinline__ float frag_rowsum(bf16x8 a, float r) {
 // ------------------------------------------------------------------------------------------------
 // bf16 MFMA kernel, 128x128 block tile
 // ------------------------------------------------------------------------------------------------
-template <int NST>
-__device__ __forceinline__ void wait_tiles(int younger) {  // this wave's DMAs of all but `younger` tiles landed
-  if (NST > 3 && younger >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if (NST > 2 && younger == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if (younger >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// this wave's DMAs of all but `younger` tiles landed (PER = DMA pieces per tile per wave)
+template <int NST, int PER = 8>
+__device__ __forceinline__ void wait_tiles(int younger) {
+  if constexpr (PER == 8) {
+    if (NST > 3 && younger >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (NST > 2 && younger == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (younger >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    static_assert(PER == 4, "wait_tiles: 4 or 8 pieces per tile");
+    if (NST > 3 && younger >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (NST > 2 && younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger >= 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
 // NST = LDS stages (K-tiles resident at once). Launched with 2 (64 KiB: two blocks per CU). Four
 // stages (three tiles in flight) on the 1-block-per-CU decoder grids measured no faster (within
 // 2 %, tools/gemm_bench.py): those blocks are bound by per-iteration latency, not DMA depth.
-template <int ALAY, int BLAY, int ACT, bool DROP, int NST>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
+template <int ALAY, int BLAY, int ACT, bool DROP, int NST, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                         long M, long N, long K, long lda, long ldb, long ldc,
                                                         int a_bytes, int b_bytes, Epi e, int ksplit, long kchunk,
                                                         float* __restrict__ ws, float* __restrict__ rowsum,
                                                         int* __restrict__ tile_cnt, long ws_bytes) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // NW = 4: waves 2 (M) x 2 (N), 64x64 each; NW = 8: 4 (M) x 2 (N), 32x64 each (MI 16-row blocks)
+  constexpr int NT = 64 * NW, WR = 128 / (NW / 2), MI = WR / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
@@ -354,33 +365,33 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 #define AS(b) (smem + (b) * 2 * TILE_BYTES)
 #define BS(b) (smem + (b) * 2 * TILE_BYTES + TILE_BYTES)
 
-  f32x4 acc[4][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // fused row sums of A (bias gradients): only the TN instance (weight-gradient GEMMs), blocks of
   // the first column tile, waves of its first column half (wave-uniform branch)
   const bool do_rs = ALAY == MIT_MN_CONTIG && BLAY == MIT_MN_CONTIG && rowsum != nullptr && bn == 0 && wn == 0;
-  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+  float rs[MI] = {};
 
   const int nk = (int)((ke - kb + BK - 1) / BK);
   auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[MI], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag<ALAY>(AS(cur), wm * 64 + i * 16, kk, lane);
+      for (int i = 0; i < MI; ++i) af[i] = frag<ALAY>(AS(cur), wm * WR + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = frag<BLAY>(BS(cur), wn * 64 + j * 16, kk, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       if (do_rs) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) rs[i] = frag_rowsum(af[i], rs[i]);
+        for (int i = 0; i < MI; ++i) rs[i] = frag_rowsum(af[i], rs[i]);
       }
     }
   };
@@ -391,17 +402,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
 #pragma unroll
   for (int t = 0; t < PF; ++t)
     if (t < nk) {
-      glds_tile<ALAY>(ra, AS(t), lda, M, ke, m0, kb + (long)t * BK, wid, lane);
-      glds_tile<BLAY>(rb, BS(t), ldb, N, ke, n0, kb + (long)t * BK, wid, lane);
+      glds_tile<ALAY, 16 / NW>(ra, AS(t), lda, M, ke, m0, kb + (long)t * BK, wid, lane);
+      glds_tile<BLAY, 16 / NW>(rb, BS(t), ldb, N, ke, n0, kb + (long)t * BK, wid, lane);
     }
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt % NST;
     if (kt + PF < nk) {  // refills the buffer computed in iteration kt-1 (behind its closing barrier)
       const int nb = (kt + PF) % NST;
-      glds_tile<ALAY>(ra, AS(nb), lda, M, ke, m0, kb + (long)(kt + PF) * BK, wid, lane);
-      glds_tile<BLAY>(rb, BS(nb), ldb, N, ke, n0, kb + (long)(kt + PF) * BK, wid, lane);
+      glds_tile<ALAY, 16 / NW>(ra, AS(nb), lda, M, ke, m0, kb + (long)(kt + PF) * BK, wid, lane);
+      glds_tile<BLAY, 16 / NW>(rb, BS(nb), ldb, N, ke, n0, kb + (long)(kt + PF) * BK, wid, lane);
     }
-    wait_tiles<NST>(min(nk - 1 - kt, PF));
+    wait_tiles<NST, 2 * (16 / NW)>(min(nk - 1 - kt, PF));
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
     compute(cur);
     __builtin_amdgcn_s_barrier();  // every wave is done reading buffer cur before it is refilled
@@ -412,21 +423,21 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
   // ---- epilogue: accumulators -> LDS (fp32 [128][CST]) -> 8-column vector rows ----
   float* cs = (float*)smem;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        cs[(wm * 64 + i * 16 + (lane >> 4) * 4 + t) * CST + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][t];
+        cs[(wm * WR + i * 16 + (lane >> 4) * 4 + t) * CST + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][t];
   if (do_rs) {
     // lanes l, l+16, l+32, l+48 hold the four k-groups of row (l & 15): reduce across them
     float* dst = ksplit > 1 ? ws + (long)ksplit * M * N + (long)split * M : rowsum;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MI; ++i) {
       float v = rs[i];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      const long r = m0 + wm * 64 + i * 16 + (lane & 15);
+      const long r = m0 + wm * WR + i * 16 + (lane & 15);
       if (lane < 16 && r < M) dst[r] = v;
     }
   }
@@ -440,8 +451,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)ws, (short)0, (int)ws_bytes, 0x00020000);
     const int slab = (split * ntiles + bid) * (BM * BN);
 #pragma unroll 4
-    for (int pass = 0; pass < (BM * BN / 4) / 256; ++pass) {
-      const int id = pass * 256 + tid;
+    for (int pass = 0; pass < (BM * BN / 4) / NT; ++pass) {
+      const int id = pass * NT + tid;
       const int r = id >> 5, c4 = (id & 31) * 4;
       const f32x4 v = *(const f32x4*)(cs + r * CST + c4);
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rw, (slab + r * BN + c4) * 4, 0, 16);
@@ -463,17 +474,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     if (!*flag) return;
   }
   if (!tile_cnt && ksplit == 1 && epi_gatherable(e)) {  // gathered epilogue: all loads, then all stores
-    constexpr int NP = (BM * BN / 8) / 256;
+    constexpr int NP = (BM * BN / 8) / NT;
     const long gc = n0 + (tid & 15) * 8;  // this thread's columns are the same in every pass
     float b[8];
     epi_bias8(e, gc, N, b);
     bf16x8 xs[NP];
 #pragma unroll
-    for (int pass = 0; pass < NP; ++pass) xs[pass] = epi_x8(e, M, N, m0 + ((pass * 256 + tid) >> 4), gc);
+    for (int pass = 0; pass < NP; ++pass) xs[pass] = epi_x8(e, M, N, m0 + ((pass * NT + tid) >> 4), gc);
     const uint64_t key = epi_key<DROP>(e);
 #pragma unroll
     for (int pass = 0; pass < NP; ++pass) {
-      const int r = (pass * 256 + tid) >> 4, c8 = (tid & 15) * 8;
+      const int r = (pass * NT + tid) >> 4, c8 = (tid & 15) * 8;
       const long gr = m0 + r;
       if (gr >= M || gc >= N) continue;
       const f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
@@ -483,8 +494,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(const bf16* __restrict__
     return;
   }
 #pragma unroll 2
-  for (int pass = 0; pass < (BM * BN / 8) / 256; ++pass) {
-    const int id = pass * 256 + tid;
+  for (int pass = 0; pass < (BM * BN / 8) / NT; ++pass) {
+    const int id = pass * NT + tid;
     const int r = id >> 4, c8 = (id & 15) * 8;
     const long gr = m0 + r, gc = n0 + c8;
     if (gr >= M || gc >= N) continue;
@@ -951,6 +962,122 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Register-streaming NT kernel for the decode step's B-row GEMMs (M = B <= 256, short K: the 128
+// kernel runs 2 x N/128 blocks through a K loop bound by per-K-step DMA issue / barrier / fragment
+// read latency). 64x64 output tile per 4-wave block; no operand staging: each wave loads
+// its MFMA fragments straight from global memory into registers (16-B buffer loads, out-of-range
+// rows / k read as 0), one K-step ahead of its MFMAs, and the four waves split K (wave w takes
+// K-steps w, w+4, ...), so the K loop has no barrier at all. The four partial tiles meet once in
+// LDS (fp32, padded rows: conflict-free), then every thread sums 16 outputs and runs the gathered
+// epilogue. Both operands K-contig (NT).
+// ------------------------------------------------------------------------------------------------
+constexpr int RS_LD = 68;                                 // fp32 row stride of a partial tile in LDS
+constexpr int RS_SMEM = 4 * 64 * RS_LD * 4;               // 4 partial 64x64 tiles (69632 B)
+
+template <int ACT, bool DROP>
+__global__ __launch_bounds__(256) void gemm_rs_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
+                                                      long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
+                                                      int b_bytes, Epi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nbn = (int)((N + 63) / 64), nbm = (int)((M + 63) / 64);
+  const int bid = xcd_remap(blockIdx.x, nbm * nbn);  // an XCD's blocks: consecutive row blocks share A
+  const int bm = bid / nbn, bn = bid % nbn;
+  const long m0 = (long)bm * 64, n0 = (long)bn * 64;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
+
+  // this lane's fragment rows (16-row block i: + 16 i) and k offset inside a 32-wide slice
+  const long ar = m0 + (lane & 15), brow = n0 + (lane & 15);
+  const int kl = 8 * (lane >> 4);
+  auto ld8 = [&](__amdgpu_buffer_rsrc_t rs, long row, long rows, long ld, long k) -> bf16x8 {
+    const uint32_t off = (row < rows && k < K) ? (uint32_t)((row * ld + k) * 2) : OOB;
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+  };
+  auto load = [&](int s, bf16x8 (&a)[4][2], bf16x8 (&b)[4][2]) {
+    const long k0 = (long)s * BK + kl;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i][kk] = ld8(ra, ar + i * 16, M, lda, k0 + kk * 32);
+        b[i][kk] = ld8(rb, brow + i * 16, N, ldb, k0 + kk * 32);
+      }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](bf16x8 (&a)[4][2], bf16x8 (&b)[4][2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+  };
+
+  const int ns = (int)((K + BK - 1) / BK);
+  bf16x8 a0[4][2], b0[4][2], a1[4][2], b1[4][2];
+  int s = w;
+  if (s < ns) load(s, a0, b0);
+  for (; s < ns; s += 8) {
+    if (s + 4 < ns) load(s + 4, a1, b1);
+    mma(a0, b0);
+    if (s + 4 >= ns) break;
+    if (s + 8 < ns) load(s + 8, a0, b0);
+    mma(a1, b1);
+  }
+
+  // the four partial tiles -> LDS, then thread t sums row t/4, columns 16 (t%4) .. +16
+  float* red = (float*)smem;
+  {
+    float* mine = red + w * 64 * RS_LD;
+    const int g = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) mine[(i * 16 + g * 4 + t) * RS_LD + j * 16 + (lane & 15)] = acc[i][j][t];
+  }
+  const int r = tid >> 2, cq = (tid & 3) * 16;
+  const long gr = m0 + r;
+  const bool gather = epi_gatherable(e);
+  float bias0[8], bias1[8];
+  bf16x8 x0 = {}, x1 = {};
+  uint64_t key = 0;
+  if (gather) {  // operand loads before the barrier (and before any store)
+    epi_bias8(e, n0 + cq, N, bias0);
+    epi_bias8(e, n0 + cq + 8, N, bias1);
+    x0 = epi_x8(e, M, N, gr, n0 + cq);
+    x1 = epi_x8(e, M, N, gr, n0 + cq + 8);
+    key = epi_key<DROP>(e);
+  }
+  __syncthreads();
+  float v[16];
+#pragma unroll
+  for (int c = 0; c < 16; c += 4) {
+    f32x4 a = *(const f32x4*)(red + r * RS_LD + cq + c);
+#pragma unroll
+    for (int q = 1; q < 4; ++q) a += *(const f32x4*)(red + (q * 64 + r) * RS_LD + cq + c);
+    v[c] = a[0];
+    v[c + 1] = a[1];
+    v[c + 2] = a[2];
+    v[c + 3] = a[3];
+  }
+  if (gr >= M) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const long gc = n0 + cq + h * 8;
+    if (gc >= N) continue;
+    if (gather) epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v + h * 8, h ? bias1 : bias0, h ? x1 : x0, key);
+    else epi_row8<ACT, DROP>(e, C, ldc, N, gr, gc, v + h * 8);
+  }
+}
+
 // C = alpha * sum_s slab[s] (f32 or bf16 out, optional accumulate); rowsum = sum_s rowslab[s]
 __global__ void gemm_splitk_reduce(long M, long N, int ksplit, const float* __restrict__ ws, void* C, long ldc,
                                    float alpha, int out_f32, int accumulate, float* rowsum) {
@@ -1099,6 +1226,26 @@ struct Split {
   bool fused = false;
 };
 
+int g_num_cus = 0;
+int num_cus() {
+  if (!g_num_cus) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    g_num_cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount : 256;
+  }
+  return g_num_cus;
+}
+int g_w8 = -1;  // 8-wave 128 kernel: 0 = off, 1 = grids of <= one block per CU, 2 = always (env MIT_GEMM_W8)
+int waves8() {
+  if (g_w8 < 0) g_w8 = getenv("MIT_GEMM_W8") ? atoi(getenv("MIT_GEMM_W8")) : 2;
+  return g_w8;
+}
+int g_deep3 = -1;
+int deep3() {
+  if (g_deep3 < 0) g_deep3 = getenv("MIT_GEMM_DEEP3") ? atoi(getenv("MIT_GEMM_DEEP3")) : 0;
+  return g_deep3;
+}
+
 template <int AL, int BL, int ACT, bool DROP>
 void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, const Split& sp, hipStream_t s) {
   const int ksplit = sp.ks;
@@ -1111,11 +1258,40 @@ void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes,
   static bool attr = false;
   if (!attr) {
     set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 2>, smem_bytes(2));
+    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 2, 8>, smem_bytes(2));
+    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 3, 8>, smem_bytes(3));
     attr = true;
+  }
+  if (waves8() && deep3() && nblk <= num_cus()) {  // (A/B knob) 3 LDS stages for <= 1 block per CU
+    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP, 3, 8>), dim3((unsigned)nblk), dim3(512), smem_bytes(3), s,
+                       (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                       b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
+    return;
+  }
+  // grids of at most one block per CU: 8 waves per block (2 per SIMD, each issuing half the LDS-DMA
+  // pieces of a K-tile) -- with one 4-wave block per CU every K-tile's 8 DMA pieces per wave sit
+  // serially in front of its 32 MFMAs
+  if (waves8() && (waves8() == 2 || nblk <= num_cus())) {
+    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP, 2, 8>), dim3((unsigned)nblk), dim3(512), smem_bytes(2), s,
+                       (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                       b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
+    return;
   }
   hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP, 2>), dim3((unsigned)nblk), dim3(256), smem_bytes(2), s,
                      (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
                      b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
+}
+
+template <int ACT, bool DROP>
+void launch_rs(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    set_lds(gemm_rs_kernel<ACT, DROP>, RS_SMEM);
+    attr = true;
+  }
+  const long nb = ((g->M + 63) / 64) * ((g->N + 63) / 64);
+  hipLaunchKernelGGL((gemm_rs_kernel<ACT, DROP>), dim3((unsigned)nb), dim3(256), RS_SMEM, s, (const bf16*)g->A,
+                     (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
 }
 
 template <int AL, int BL, int ACT, bool DROP>
@@ -1137,6 +1313,21 @@ int g_variant = -1;
 int gemm_variant() {
   if (g_variant < 0) g_variant = getenv("MIT_GEMM_VARIANT") ? atoi(getenv("MIT_GEMM_VARIANT")) : 0;
   return g_variant;
+}
+
+// register-streaming kernel (gemm_rs_kernel): the decode step's B-row GEMMs (M <= 256) with a short
+// K and N <= 2048 -- 7.2 vs 9.9 us per launch on 256 x {512, 1536, 2048} x 512. Everywhere else it
+// loses: each wave streams its own A and B fragments from L2 (8 FLOP per L2 byte vs 64 for the 128
+// kernel's LDS tiles): 2.5-3x slower on the M = 4032 decoder shapes, 2x on the decode fc_out
+// (tools/blas_reference.py, MIT_GEMM_RS=0 turns it off)
+int g_rs = -1;
+bool use_rs(const mit_gemm_args* g) {
+  if (g_rs < 0) g_rs = getenv("MIT_GEMM_RS") ? atoi(getenv("MIT_GEMM_RS")) : 1;
+  if (g->a_layout != MIT_K_CONTIG || g->b_layout != MIT_K_CONTIG || g->rowsum) return false;
+  const int v = gemm_variant();
+  if (v == 3) return true;
+  if (!g_rs || v != 0) return false;
+  return g->M <= 256 && g->N <= 2048 && g->K <= 1024;
 }
 
 // Occupancy-quantised cost model: the 128x128 kernel runs 2 blocks per CU, the 256x256 kernel 1;
@@ -1172,6 +1363,18 @@ EpiKind epi_kind(const mit_gemm_args* g) {
 template <int AL, int BL>
 void launch_layout(const mit_gemm_args* g, const Epi& e, int ab, int bb, const Split& sp, bool big, hipStream_t s) {
   const EpiKind k = epi_kind(g);
+  if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
+    if (sp.ks == 1 && use_rs(g)) {
+      switch (k) {
+        case EK_PLAIN: return launch_rs<MIT_ACT_NONE, false>(g, e, ab, bb, s);
+        case EK_RELU: return launch_rs<MIT_ACT_RELU, false>(g, e, ab, bb, s);
+        case EK_RELU_DROP: return launch_rs<MIT_ACT_RELU, true>(g, e, ab, bb, s);
+        case EK_GELU: return launch_rs<MIT_ACT_GELU, false>(g, e, ab, bb, s);
+        case EK_QGELU: return launch_rs<MIT_ACT_QUICK_GELU, false>(g, e, ab, bb, s);
+        default: return launch_rs<ACT_RT, true>(g, e, ab, bb, s);
+      }
+    }
+  }
   if (big && k != EK_GENERIC) {
     if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
       switch (k) {
@@ -1242,7 +1445,7 @@ Split plan_split(const mit_gemm_args* g) {
 }  // namespace
 
 extern "C" int mit_gemm_set_variant(int v) {
-  MIT_CHECK_ARG(v >= 0 && v <= 2, "mit_gemm_set_variant: %d not in {0,1,2}", v);
+  MIT_CHECK_ARG(v >= 0 && v <= 3, "mit_gemm_set_variant: %d not in {0,1,2,3}", v);
   g_variant = v;
   return MIT_OK;
 }
@@ -1266,6 +1469,7 @@ extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
   if (g->dtype != MIT_BF16) return 64;
   const Split sp = plan_split(g);
   if (ksplit) *ksplit = sp.ks;
+  if (sp.ks == 1 && use_rs(g)) return 65;  // the 64x64 register-streaming kernel
   const bool big = sp.ks == 1 && use_256(g->M, g->N, g->K, g->a_layout) && epi_kind(g) != EK_GENERIC;
   return big ? 256 : 128;
 }

@@ -166,3 +166,40 @@ def test_gemm_split_k_in_launch_combine(al, bl, M, Nn, K, epi):
     scale = max(outs[0].float().abs().max().item(), 1.0)
     assert d <= (2e-2 if out_dt == torch.bfloat16 else 1e-4) * scale, d
 
+
+
+@pytest.mark.parametrize("M,Nn,K", [(4032, 512, 512), (4032, 512, 2048), (256, 10000, 512), (250, 520, 200),
+                                    (1000, 136, 1096), (64, 64, 64), (70, 2048, 72)])
+def test_register_streaming_kernel(M, Nn, K):
+    """The 64x64 register-streaming NT kernel (gemm_rs_kernel, variant 3) against fp32 torch and the
+    128 kernel: ragged M / N / K edges, K split over the four waves, every fused epilogue."""
+    A, B, ref = _ops(M, Nn, K, 0, 0, seed=M + Nn + K)
+    N.gemm_set_variant(3)
+    C = torch.empty(M, Nn, device=dev(), dtype=torch.float32)
+    N.gemm(A, B, C, M, Nn, K)
+    assert _rel(C, ref) < 1e-5
+    g = torch.Generator().manual_seed(9)
+    bias = torch.randn(Nn, generator=g).to(dev())
+    res = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
+    aux = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
+    seed = torch.tensor([7], dtype=torch.int64, device=dev())
+    cases = [dict(bias=bias, act=a, residual=res) for a in (N.ACT_RELU, N.ACT_GELU, N.ACT_QUICK_GELU)]
+    cases += [dict(bias=bias, act=N.ACT_RELU, drop_p=0.1, seed=seed, site=5), dict(aux=aux, aux_scale=1.5),
+              dict(residual=res, aux=aux, aux_scale=2.0)]
+    for kw in cases:
+        outs = []
+        for v in (3, 1):
+            N.gemm_set_variant(v)
+            out = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
+            N.gemm(A, B, out, M, Nn, K, **kw)
+            outs.append(out.float())
+        scale = outs[1].abs().max().item()
+        assert (outs[0] - outs[1]).abs().max().item() <= 1e-2 * max(scale, 1.0), kw
+    acc0 = torch.randn(M, Nn, generator=g).to(dev())
+    N.gemm_set_variant(3)
+    acc = acc0.clone()
+    N.gemm(A, B, acc, M, Nn, K, alpha=0.5, accumulate=True)
+    assert _rel(acc, acc0 + 0.5 * ref) < 1e-5
+    C2 = torch.empty_like(C)
+    N.gemm(A, B, C2, M, Nn, K)
+    assert torch.equal(C, C2), "register-streaming kernel not deterministic"

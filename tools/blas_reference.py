@@ -11,7 +11,8 @@ import torch  # noqa: E402
 
 import native  # noqa: E402
 
-# name, M, N, K, a_layout, b_layout (0 = K-contig, 1 = MN-contig), count per step
+# name, M, N, K, a_layout, b_layout (0 = K-contig, 1 = MN-contig), count per step ("dec1": one
+# token step of the configs[4] batched decode, B = 256 rows; not part of the train-step sum)
 SHAPES = [
     ("enc qkv", 12608, 2304, 768, 0, 0, 12), ("enc o+res", 12608, 768, 768, 0, 0, 12),
     ("enc fc1+gelu", 12608, 3072, 768, 0, 0, 12), ("enc fc2+res", 12608, 768, 3072, 0, 0, 12),
@@ -24,6 +25,9 @@ SHAPES = [
     ("dW d-d", 512, 512, 4032, 1, 1, 18), ("dW ffn1", 2048, 512, 4032, 1, 1, 6),
     ("dW ffn2", 512, 2048, 4032, 1, 1, 6), ("dW self_in", 1536, 512, 4032, 1, 1, 6),
     ("dW fc_out", 10000, 512, 4032, 1, 1, 1), ("dW kv_all", 6144, 512, 12608, 1, 1, 1),
+    ("dec1 self_in", 256, 1536, 512, 0, 0, 6), ("dec1 d-out", 256, 512, 512, 0, 0, 18),
+    ("dec1 ffn1", 256, 2048, 512, 0, 0, 6), ("dec1 ffn2", 256, 512, 2048, 0, 0, 6),
+    ("dec1 fc_out", 256, 10000, 512, 0, 0, 1),
     ("4096^3", 4096, 4096, 4096, 0, 0, 0),
 ]
 
@@ -68,8 +72,9 @@ def main():
             tb.append(timeit(blas))
         to, tb = min(to), min(tb)
         fl = 2.0 * M * N * K
-        tot_ours += cnt * to
-        tot_blas += cnt * tb
+        if not name.startswith("dec1"):
+            tot_ours += cnt * to
+            tot_blas += cnt * tb
         print(f"{name:14s} {M:6d} {N:6d} {K:6d}  {to:8.1f} {fl / to / 1e6:6.0f}  {tb:12.1f} {fl / tb / 1e6:6.0f}  {tb / to:5.2f}",
               flush=True)
     print(f"per-step GEMM sum (isolated, x count): ours {tot_ours / 1e3:.3f} ms, hipBLASLt {tot_blas / 1e3:.3f} ms")
