@@ -1240,11 +1240,6 @@ int waves8() {
   if (g_w8 < 0) g_w8 = getenv("MIT_GEMM_W8") ? atoi(getenv("MIT_GEMM_W8")) : 2;
   return g_w8;
 }
-int g_deep3 = -1;
-int deep3() {
-  if (g_deep3 < 0) g_deep3 = getenv("MIT_GEMM_DEEP3") ? atoi(getenv("MIT_GEMM_DEEP3")) : 0;
-  return g_deep3;
-}
 
 template <int AL, int BL, int ACT, bool DROP>
 void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, const Split& sp, hipStream_t s) {
@@ -1259,14 +1254,7 @@ void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes,
   if (!attr) {
     set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 2>, smem_bytes(2));
     set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 2, 8>, smem_bytes(2));
-    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 3, 8>, smem_bytes(3));
     attr = true;
-  }
-  if (waves8() && deep3() && nblk <= num_cus()) {  // (A/B knob) 3 LDS stages for <= 1 block per CU
-    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP, 3, 8>), dim3((unsigned)nblk), dim3(512), smem_bytes(3), s,
-                       (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                       b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
-    return;
   }
   // grids of at most one block per CU: 8 waves per block (2 per SIMD, each issuing half the LDS-DMA
   // pieces of a K-tile) -- with one 4-wave block per CU every K-tile's 8 DMA pieces per wave sit
