@@ -247,6 +247,9 @@ long mit_colsum_ws_floats(long M, long N);
 long mit_grad_norm_ws_floats(long n);
 int mit_grad_norm(const float* grads, long n, float max_norm, float* ws, float* norm_out, void* stream);
 int mit_step_inc(int64_t* step, void* stream);
+/* Profiling marker: buf[idx] = the device's constant-rate wall clock (hipDeviceAttributeWallClockRate)
+ * when the stream reaches this point. Recorded into launch plans like any launch. */
+int mit_stamp(uint64_t* buf, int idx, void* stream);
 int mit_adamw(long n, float* param, const float* grad, float* m, float* v, void* shadow_bf16, const float* norm_out,
               const float* lr, const int64_t* step, float beta1, float beta2, float eps, float weight_decay,
               void* stream);

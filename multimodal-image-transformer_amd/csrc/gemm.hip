@@ -1108,11 +1108,13 @@ __global__ void gemm_splitk_reduce(long M, long N, int ksplit, const float* __re
 
 // split-K plan for a plain-epilogue bf16 GEMM: only when the output has too few 128x128 tiles to
 // fill 256 CUs and K is long (the weight-gradient shapes). Returns 1 (no split) otherwise.
+int g_split_target = -1;  // blocks the split aims for (env MIT_SPLITK_TARGET; 128 beat 512 / 256 / 64 by 0.8-4 % in the step: fewer fp32 slabs)
 int splitk_plan(long M, long N, long K, long* kchunk) {
   const long tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   *kchunk = K;
+  if (g_split_target < 0) g_split_target = getenv("MIT_SPLITK_TARGET") ? atoi(getenv("MIT_SPLITK_TARGET")) : 128;
   if (tiles >= 256 || K < 1024 || N % 8) return 1;
-  long s = (512 + tiles - 1) / tiles;
+  long s = (g_split_target + tiles - 1) / tiles;
   s = min(s, K / 512);
   s = min(s, 16L);
   if (s < 2) return 1;

@@ -379,6 +379,9 @@ __global__ void norm_final(const float* __restrict__ ws, int nb, float max_norm,
   }
 }
 __global__ void step_inc_kernel(int64_t* step) { *step += 1; }
+// stream timestamp: the constant-rate device clock (wall_clock64, hipDeviceAttributeWallClockRate)
+// when this point of the stream is reached (phase timing of a recorded step, tools/phase_timing.py)
+__global__ void stamp_kernel(uint64_t* out, int i) { out[i] = wall_clock64(); }
 __global__ void scalar_div_kernel(const float* a, const float* b, float* out) { *out = *a / *b; }
 
 template <bool SHADOW>
@@ -624,6 +627,14 @@ extern "C" int mit_grad_norm(const float* grads, long n, float max_norm, float* 
   MIT_LAUNCH_CHECK("mit_grad_norm");
   hipLaunchKernelGGL(norm_final, dim3(1), dim3(256), 0, s, ws, GN_BLOCKS, max_norm, norm_out);
   MIT_LAUNCH_CHECK("mit_grad_norm(final)");
+  return MIT_OK;
+}
+
+extern "C" int mit_stamp(uint64_t* buf, int idx, void* stream) {
+  MIT_RECORD([=]() { return mit_stamp(buf, idx, stream); });
+  MIT_CHECK_ARG(buf && idx >= 0, "mit_stamp: null buffer or negative index");
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, buf, idx);
+  MIT_LAUNCH_CHECK("mit_stamp");
   return MIT_OK;
 }
 

@@ -85,6 +85,7 @@ SIGNATURES = {
     "mit_grad_norm_ws_floats": (L, [L]),
     "mit_grad_norm": (I, [vp, L, Fl, vp, vp, vp]),
     "mit_step_inc": (I, [vp, vp]),
+    "mit_stamp": (I, [vp, I, vp]),
     "mit_adamw": (I, [L, vp, vp, vp, vp, vp, vp, vp, vp, Fl, Fl, Fl, Fl, vp]),
     "mit_cast_f32": (I, [I, L, vp, vp, vp]),
     "mit_zero": (I, [vp, L, vp]),
@@ -490,6 +491,11 @@ def grad_norm_ws_floats(n):
 def grad_norm(grads, max_norm, ws, norm_out):
     _check(lib().mit_grad_norm(ptr(grads), grads.numel(), max_norm, ptr(ws), ptr(norm_out), stream_ptr()),
            "mit_grad_norm")
+
+
+def stamp(buf: torch.Tensor, idx: int, stream=None):
+    """buf[idx] (int64 device tensor) = device wall clock when `stream` (default: current) gets here."""
+    _check(lib().mit_stamp(ptr(buf), int(idx), stream if stream is not None else stream_ptr()), "mit_stamp")
 
 
 def step_inc(step):
