@@ -258,7 +258,10 @@ class DecodeState:
         self.pos = torch.zeros(1, dtype=torch.int64, device=dev)
         self.finished = torch.zeros(B, dtype=torch.int32, device=dev)
         self.n_finished = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.kv = torch.empty(B * S, L * 2 * d, dtype=dt, device=dev)
+        # per layer contiguous [L][B*S][2d] (K | V): a decode attention block (b, h) then reads its S keys
+        # at a 2 KiB stride instead of the training layout's L * 2d row (12 KiB at cfg1), which left the
+        # S = 197 cross attention at ~2.6 TB/s on DRAM page misses
+        self.kv = torch.empty(L, B * S, 2 * d, dtype=dt, device=dev)
         self.cache = [torch.empty(B, max_len, 2 * d, dtype=dt, device=dev) for _ in range(L)]
         e = lambda n: torch.empty(B, n, dtype=dt, device=dev)  # noqa: E731
         self.x, self.x1, self.x2, self.y, self.o, self.q = e(d), e(d), e(d), e(d), e(d), e(d)
@@ -581,7 +584,9 @@ class TransformerDecoder:
                              f"decoder_max_seq_len; the reference's PositionalEncoding would fail too)")
         stt = DecodeState(self, B, S, max_len, start_id, end_id)
         d, L, st = self.d, self.L, self.store
-        native.gemm(mem, st.w("cross_kv.weight"), stt.kv, B * S, L * 2 * d, d, lda=mem_ld, bias=st.p("cross_kv.bias"))
+        wkv, bkv = st.w("cross_kv.weight"), st.p("cross_kv.bias")
+        for l in range(L):
+            native.gemm(mem, wkv[l * 2 * d:], stt.kv[l], B * S, 2 * d, d, lda=mem_ld, bias=bkv[l * 2 * d:])
         return stt
 
     def decode_step(self, stt: "DecodeState"):
@@ -603,8 +608,8 @@ class TransformerDecoder:
             native.linear(stt.o, w(pre + "self_out.weight"), stt.y, bias=st.p(pre + "self_out.bias"))
             native.layernorm_fwd(x, st.p(pre + "norm1.weight"), st.p(pre + "norm1.bias"), 1e-5, stt.x1, r=stt.y)
             native.linear(stt.x1, w(pre + "cross_q.weight"), stt.q, bias=st.p(pre + "cross_q.bias"))
-            kvl = stt.kv[:, l * 2 * d:]
-            native.attention_decode(stt.q, d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d, S * L * 2 * d,
+            kvl = stt.kv[l]
+            native.attention_decode(stt.q, d, kvl, 2 * d, S * 2 * d, kvl[:, d:], 2 * d, S * 2 * d,
                                     stt.o, d, B, H, Lk=S, scale=1.0 / math.sqrt(self.hd), Dh=self.hd)
             native.linear(stt.o, w(pre + "cross_out.weight"), stt.y, bias=st.p(pre + "cross_out.bias"))
             native.layernorm_fwd(stt.x1, st.p(pre + "norm2.weight"), st.p(pre + "norm2.bias"), 1e-5, stt.x2, r=stt.y)
