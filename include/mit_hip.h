@@ -280,6 +280,56 @@ int mit_embed_decode(int dtype, long B, long d, const int64_t* ids, long ld_ids,
                      float scale, const float* pe, void* out, void* stream);
 int mit_greedy_pick(long B, long V, const float* logits, long ld, int64_t* ids, long ld_ids, const int64_t* pos,
                     int64_t end_id, int64_t pad_id, int* finished, int* n_finished, void* stream);
+/* greedy_pick, then *pos += 1 once every row's pick is stored (the last block to take `ticket`, an
+ * int32 device counter that must start at 0 and is left at 0, advances it): the per-token step's
+ * separate mit_step_inc launch folded in. */
+int mit_greedy_pick_advance(long B, long V, const float* logits, long ld, int64_t* ids, long ld_ids, int64_t* pos,
+                            int64_t end_id, int64_t pad_id, int* finished, int* n_finished, int* ticket, void* stream);
+
+/* Decode-step GEMM with the decoder's post-LN residual blocks folded in (bf16 only; the B-row GEMMs of
+ * one token step, torch/nn/modules/transformer.py:1144-1153 norm_first=False):
+ *   C[M, N] = act(A'[M, K] . B[N, K]^T + bias) (+ residual),  B = bf16 weights (nn.Linear layout)
+ *   A' = A (bf16 rows, a_stats == NULL) or LN(A) with A = f32 pre-LN sums z and a_stats their row
+ *        statistics as written by a producer's stats_out, gamma/beta f32 [K] (K <= 1024);
+ *   residual (r_mode): 0 none, 1 bf16 rows r, 2 LN(r) with r = f32 pre-LN sums, r_stats, gamma/beta [N];
+ *   outputs: C (bf16, or f32 when c_f32 -- the vocabulary head), z_out f32 (the pre-LN sum of the
+ *   NEXT LayerNorm) with stats_out [M][ceil(N/64)][2] = per 64-column tile (mean, M2) of each row,
+ *   merged exactly by the consumer (Chan); cache (bf16, may be NULL): for columns n >= kv_col0,
+ *   cache[m*c_batch + (*pos)*c_row + n - kv_col0] = C value (the self-attention K|V row of this token).
+ * LayerNorm eps = eps for both A and the residual. ReLU only without a residual. */
+typedef struct {
+  long M, N, K;
+  const void* A;
+  long lda;
+  const float* a_stats;
+  const float* a_gamma;
+  const float* a_beta;
+  const void* B;
+  long ldb;
+  const float* bias;
+  int act;
+  int c_f32;
+  void* C;
+  long ldc;
+  int r_mode;
+  const void* r;
+  long ldr;
+  const float* r_stats;
+  const float* r_gamma;
+  const float* r_beta;
+  float eps;
+  float* z_out;
+  long ldz;
+  float* stats_out;
+  void* cache;
+  long c_row, c_batch, kv_col0;
+  const int64_t* pos;
+} mit_decode_gemm_args;
+int mit_decode_gemm(const mit_decode_gemm_args* args, void* stream);
+/* out[m, :] = LN(z[m, :]) (bf16) from the statistics a mit_decode_gemm stats_out wrote (W <= 1024):
+ * the vocabulary head's operand, which then runs on mit_gemm. */
+int mit_decode_layernorm(long M, long W, const float* z, long ldz, const float* stats, const float* gamma,
+                         const float* beta, float eps, void* out, long ldo, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Utilities. cast: f32 -> operand dtype copy (weights to the bf16 shadow); fill f32.

@@ -165,7 +165,8 @@ __global__ __launch_bounds__(256) void greedy_pick_kernel(long V, const float* _
                                                           int64_t* __restrict__ ids, long ld_ids,
                                                           const int64_t* __restrict__ pos, int64_t end_id,
                                                           int64_t pad_id, int* __restrict__ finished,
-                                                          int* __restrict__ n_finished) {
+                                                          int* __restrict__ n_finished, int* __restrict__ ticket,
+                                                          int64_t* __restrict__ pos_adv) {
   __shared__ float sv[4];
   __shared__ long si[4];
   const long b = blockIdx.x;
@@ -217,6 +218,330 @@ __global__ __launch_bounds__(256) void greedy_pick_kernel(long V, const float* _
         atomicAdd(n_finished, 1);
       }
     }
+    // position advance folded in (was its own launch): the ids store above consumed *pos, so when the
+    // last row's block takes the ticket every block has read the old position
+    if (ticket && atomicAdd(ticket, 1) == (int)gridDim.x - 1) {
+      *pos_adv = p + 1;
+      *ticket = 0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Decode-step GEMM with the post-LN residual blocks folded in (bf16 step only). The per-token step
+// of the 6-layer decoder was 76 launches, 24 of them tiny (LayerNorm, kv_store, step_inc: 4-5 us
+// each for ~0.5 MB of traffic). Here a LayerNorm is never its own launch:
+//  * the PRODUCER of a pre-LN sum z = A W^T + b + residual writes z in f32 plus, per 64-column tile,
+//    each row's (mean, M2) over those columns (Chan's parallel form: merged exactly, in a fixed order,
+//    by the consumer -- no atomics, deterministic);
+//  * a CONSUMER whose operand is LN(z) merges the row statistics and normalises z while staging its
+//    64 A rows into LDS (a_stats != NULL), and a residual LN(z) is applied element-wise in the
+//    epilogue (r_mode 2);
+//  * the self-attention in_proj writes its K|V columns straight into the cache row at *pos.
+// 64x64 output tile per 4-wave block; B fragments streamed from global one K-step ahead (as in
+// gemm_rs_kernel), waves split K, partial tiles summed once in LDS.
+// ------------------------------------------------------------------------------------------------
+constexpr int DG_BK = 64;
+constexpr int DG_RLD = 68;                          // fp32 row stride of a partial tile in LDS
+constexpr int DG_RED = 4 * 64 * DG_RLD * 4;         // 69632 B
+constexpr uint32_t DG_OOB = 0x80000000u;
+
+__device__ __forceinline__ int dg_xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, rr = nwg % 8, x = bid % 8, y = bid / 8;
+  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + y;
+}
+
+// merge the per-64-column (mean, M2) partials of one row of width W -> (mean, rstd); all partial loads
+// issued before the first use (W <= 64 * DG_PMAX)
+constexpr int DG_PMAX = 16;
+__device__ __forceinline__ void dg_row_stats(const float* __restrict__ st, long W, float eps, float& mean, float& rstd) {
+  const int P = (int)((W + 63) / 64);
+  f32x2 part[DG_PMAX];
+#pragma unroll
+  for (int p = 0; p < DG_PMAX; ++p) part[p] = p < P ? *(const f32x2*)(st + 2 * p) : f32x2{0.f, 0.f};
+  float s = 0.f;
+#pragma unroll
+  for (int p = 0; p < DG_PMAX; ++p) s += part[p][0] * (float)max(0L, min(64L, W - 64L * p));
+  mean = s / (float)W;
+  float m2 = 0.f;
+#pragma unroll
+  for (int p = 0; p < DG_PMAX; ++p) {
+    const float dm = part[p][0] - mean;
+    m2 += part[p][1] + dm * dm * (float)max(0L, min(64L, W - 64L * p));
+  }
+  rstd = rsqrtf(m2 / (float)W + eps);
+}
+
+template <int AMODE, int ACT, int RMODE, bool CF32>
+__global__ __launch_bounds__(256) void decode_gemm_kernel(mit_decode_gemm_args g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long M = g.M, N = g.N, K = g.K;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nbn = (int)((N + 63) / 64), nbm = (int)((M + 63) / 64);
+  const int bid = dg_xcd_remap(blockIdx.x, nbm * nbn);  // an XCD's blocks: consecutive column blocks of a row block
+  const int bm = bid / nbn, bn = bid % nbn;
+  const long m0 = (long)bm * 64, n0 = (long)bn * 64;
+  const int b_bytes = (int)(2 * ((N - 1) * g.ldb + K));
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, b_bytes, 0x00020000);
+  const long brow = n0 + (lane & 15);
+  const int kl = 8 * (lane >> 4);
+  auto ldb8 = [&](long row, long k) -> bf16x8 {
+    const uint32_t off = (row < N && k < K) ? (uint32_t)((row * g.ldb + k) * 2) : DG_OOB;
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, (int)off, 0, 0));
+  };
+  auto loadb = [&](int s, bf16x8 (&b)[4][2]) {
+    const long k0 = (long)s * DG_BK + kl;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[i][kk] = ldb8(brow + i * 16, k0 + kk * 32);
+  };
+  const int ns = (int)((K + DG_BK - 1) / DG_BK);
+  bf16x8 b0[4][2], b1[4][2];
+  int s = w;
+  if (s < ns) loadb(s, b0);
+
+  // A operand: bf16 rows straight from global (AMODE 0), or LN(z) rows staged in LDS (AMODE 1)
+  const long alda = AMODE ? (K * 2 + 16) : 0;  // LDS row stride (bytes): 16-B pad -> conflict-free reads
+  __amdgpu_buffer_rsrc_t ra;
+  if constexpr (AMODE == 0) {
+    const int a_bytes = (int)(2 * ((M - 1) * g.lda + K));
+    ra = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, a_bytes, 0x00020000);
+  } else {
+    float* st = (float*)(smem + 64 * alda);  // (mean, rstd) of the block's 64 rows
+    if (tid < 64) {
+      float mu = 0.f, rs = 0.f;
+      if (m0 + tid < M) dg_row_stats(g.a_stats + (m0 + tid) * 2 * ((K + 63) / 64), K, g.eps, mu, rs);
+      st[2 * tid] = mu;
+      st[2 * tid + 1] = rs;
+    }
+    __syncthreads();
+    // wave w normalises rows 16w .. 16w+15; lane l owns columns 8l .. 8l+7 (+512 per pass): one
+    // wave instruction reads 2 KiB of a row, and 8 rows' loads are in flight before the first store
+    for (long k = 8L * lane; k < K; k += 512) {
+      const f32x4 g0 = *(const f32x4*)(g.a_gamma + k), g1 = *(const f32x4*)(g.a_gamma + k + 4);
+      const f32x4 e0 = *(const f32x4*)(g.a_beta + k), e1 = *(const f32x4*)(g.a_beta + k + 4);
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        f32x4 z[8][2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = w * 16 + half * 8 + i;
+          if (m0 + r < M) {
+            const float* zr = (const float*)g.A + (m0 + r) * g.lda + k;
+            z[i][0] = *(const f32x4*)zr;
+            z[i][1] = *(const f32x4*)(zr + 4);
+          } else {
+            z[i][0] = z[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = w * 16 + half * 8 + i;
+          const float mu = st[2 * r], rs = st[2 * r + 1];
+          bf16x8 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            o[j] = (bf16)((z[i][0][j] - mu) * rs * g0[j] + e0[j]);
+            o[j + 4] = (bf16)((z[i][1][j] - mu) * rs * g1[j] + e1[j]);
+          }
+          *(bf16x8*)(smem + r * alda + k * 2) = o;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  auto loada = [&](int s, bf16x8 (&a)[4][2]) {
+    const long k0 = (long)s * DG_BK + kl;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long k = k0 + kk * 32;
+        if constexpr (AMODE == 0) {
+          const long row = m0 + i * 16 + (lane & 15);
+          const uint32_t off = (row < M && k < K) ? (uint32_t)((row * g.lda + k) * 2) : DG_OOB;
+          a[i][kk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)off, 0, 0));
+        } else {
+          const int row = i * 16 + (lane & 15);
+          a[i][kk] = k < K ? *(const bf16x8*)(smem + row * alda + k * 2) : bf16x8{};
+        }
+      }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](bf16x8 (&a)[4][2], bf16x8 (&b)[4][2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+  };
+  {  // both operands one K-step ahead of the MFMAs (wave w: K-steps w, w+4, ...)
+    bf16x8 a0[4][2], a1[4][2];
+    if (s < ns) loada(s, a0);
+    for (; s < ns; s += 8) {
+      if (s + 4 < ns) {
+        loada(s + 4, a1);
+        loadb(s + 4, b1);
+      }
+      mma(a0, b0);
+      if (s + 4 >= ns) break;
+      if (s + 8 < ns) {
+        loada(s + 8, a0);
+        loadb(s + 8, b0);
+      }
+      mma(a1, b1);
+    }
+  }
+  if constexpr (AMODE == 1) __syncthreads();  // the reduction below reuses the staged A's LDS
+
+  float* red = (float*)smem;
+  {
+    float* mine = red + w * 64 * DG_RLD;
+    const int gq = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) mine[(i * 16 + gq * 4 + t) * DG_RLD + j * 16 + (lane & 15)] = acc[i][j][t];
+  }
+  const int r = tid >> 2, cq = (tid & 3) * 16;
+  const long gr = m0 + r;
+  const bool rok = gr < M;
+  // epilogue operands before the barrier
+  float bias[16], res[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) bias[c] = res[c] = 0.f;
+  if (g.bias) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) bias[c] = n0 + cq + c < N ? g.bias[n0 + cq + c] : 0.f;
+  }
+  if constexpr (RMODE == 1) {
+    if (rok) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (n0 + cq + 8 * h < N) {
+          const bf16x8 x = *(const bf16x8*)((const bf16*)g.r + gr * g.ldr + n0 + cq + 8 * h);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) res[8 * h + i] = (float)x[i];
+        }
+    }
+  } else if constexpr (RMODE == 2) {
+    if (rok) {
+      float mu, rs;
+      dg_row_stats(g.r_stats + gr * 2 * ((N + 63) / 64), N, g.eps, mu, rs);
+      const float* zr = (const float*)g.r + gr * g.ldr;
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        const long gc = n0 + cq + c;
+        if (gc < N) {
+          const f32x4 z = *(const f32x4*)(zr + gc), ga = *(const f32x4*)(g.r_gamma + gc),
+                      be = *(const f32x4*)(g.r_beta + gc);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) res[c + i] = (z[i] - mu) * rs * ga[i] + be[i];
+        }
+      }
+    }
+  }
+  const long p = g.cache ? *g.pos : 0;
+  __syncthreads();
+  float v[16];
+#pragma unroll
+  for (int c = 0; c < 16; c += 4) {
+    f32x4 a = *(const f32x4*)(red + r * DG_RLD + cq + c);
+#pragma unroll
+    for (int q = 1; q < 4; ++q) a += *(const f32x4*)(red + (q * 64 + r) * DG_RLD + cq + c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x = a[i] + bias[c + i];
+      if (ACT == MIT_ACT_RELU) x = fmaxf(x, 0.f);
+      v[c + i] = x + res[c + i];
+    }
+  }
+  if (g.stats_out) {  // this tile's (mean, M2) per row over its valid columns; 4 lanes per row
+    const int nv = (int)min(64L, N - n0);
+    float sm = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) sm += (cq + c < nv) ? v[c] : 0.f;
+    sm += __shfl_xor(sm, 1, 64);
+    sm += __shfl_xor(sm, 2, 64);
+    const float mp = sm / (float)nv;
+    float q2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float dv = v[c] - mp;
+      q2 += (cq + c < nv) ? dv * dv : 0.f;
+    }
+    q2 += __shfl_xor(q2, 1, 64);
+    q2 += __shfl_xor(q2, 2, 64);
+    if (rok && (tid & 3) == 0) {
+      float* so = g.stats_out + (gr * nbn + bn) * 2;
+      so[0] = mp;
+      so[1] = q2;
+    }
+  }
+  if (!rok) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const long gc = n0 + cq + 8 * h;
+    if (gc >= N) continue;
+    const float* vv = v + 8 * h;
+    if (g.C) {
+      if constexpr (CF32) {
+        float* o = (float*)g.C + gr * g.ldc + gc;
+        *(f32x4*)o = f32x4{vv[0], vv[1], vv[2], vv[3]};
+        *(f32x4*)(o + 4) = f32x4{vv[4], vv[5], vv[6], vv[7]};
+      } else {
+        bf16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (bf16)vv[i];
+        *(bf16x8*)((bf16*)g.C + gr * g.ldc + gc) = o;
+      }
+    }
+    if (g.z_out) {
+      float* o = g.z_out + gr * g.ldz + gc;
+      *(f32x4*)o = f32x4{vv[0], vv[1], vv[2], vv[3]};
+      *(f32x4*)(o + 4) = f32x4{vv[4], vv[5], vv[6], vv[7]};
+    }
+    if (g.cache && gc >= g.kv_col0) {
+      bf16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (bf16)vv[i];
+      *(bf16x8*)((bf16*)g.cache + gr * g.c_batch + p * g.c_row + (gc - g.kv_col0)) = o;
+    }
+  }
+}
+
+// out[m, :] = LN(z[m, :]) in bf16 from the producer's row statistics: the vocabulary head's operand
+// (a 10000-column head re-staging LN rows per 64-column block cost 45 us; this + the 128 GEMM ~13)
+__global__ __launch_bounds__(256) void decode_ln_kernel(long M, long W, const float* __restrict__ z, long ldz,
+                                                        const float* __restrict__ stats, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps, bf16* __restrict__ out,
+                                                        long ldo) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= M) return;
+  float mu, rs;
+  dg_row_stats(stats + r * 2 * ((W + 63) / 64), W, eps, mu, rs);
+  for (long k = 8L * lane; k < W; k += 512) {
+    const float* zr = z + r * ldz + k;
+    const f32x4 z0 = *(const f32x4*)zr, z1 = *(const f32x4*)(zr + 4);
+    const f32x4 g0 = *(const f32x4*)(gamma + k), g1 = *(const f32x4*)(gamma + k + 4);
+    const f32x4 e0 = *(const f32x4*)(beta + k), e1 = *(const f32x4*)(beta + k + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (bf16)((z0[j] - mu) * rs * g0[j] + e0[j]);
+      o[j + 4] = (bf16)((z1[j] - mu) * rs * g1[j] + e1[j]);
+    }
+    *(bf16x8*)(out + r * ldo + k) = o;
   }
 }
 
@@ -301,7 +626,100 @@ extern "C" int mit_greedy_pick(long B, long V, const float* logits, long ld, int
   MIT_CHECK_ARG(logits && ids && pos && finished && n_finished && ld >= V && V > 0, "mit_greedy_pick: bad arguments");
   if (B <= 0) return MIT_OK;
   hipLaunchKernelGGL(greedy_pick_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, V, logits, ld, ids,
-                     ld_ids, pos, end_id, pad_id, finished, n_finished);
+                     ld_ids, pos, end_id, pad_id, finished, n_finished, (int*)nullptr, (int64_t*)nullptr);
   MIT_LAUNCH_CHECK("mit_greedy_pick");
+  return MIT_OK;
+}
+
+extern "C" int mit_greedy_pick_advance(long B, long V, const float* logits, long ld, int64_t* ids, long ld_ids,
+                                       int64_t* pos, int64_t end_id, int64_t pad_id, int* finished, int* n_finished,
+                                       int* ticket, void* stream) {
+  MIT_RECORD([=]() { return mit_greedy_pick_advance(B, V, logits, ld, ids, ld_ids, pos, end_id, pad_id, finished, n_finished, ticket, stream); });
+  MIT_CHECK_ARG(logits && ids && pos && finished && n_finished && ticket && ld >= V && V > 0,
+                "mit_greedy_pick_advance: bad arguments");
+  MIT_CHECK_ARG(B > 0 && B < (1L << 30), "mit_greedy_pick_advance: B = %ld", B);
+  hipLaunchKernelGGL(greedy_pick_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, V, logits, ld, ids,
+                     ld_ids, pos, end_id, pad_id, finished, n_finished, ticket, pos);
+  MIT_LAUNCH_CHECK("mit_greedy_pick_advance");
+  return MIT_OK;
+}
+
+namespace {
+template <int AMODE, int ACT, int RMODE, bool CF32>
+int launch_decode_gemm(const mit_decode_gemm_args* g, hipStream_t s) {
+  const long nblk = ((g->M + 63) / 64) * ((g->N + 63) / 64);
+  const int lds = AMODE ? (int)max(64L * (g->K * 2 + 16) + 512, (long)DG_RED) : DG_RED;
+  static int attr = 0;
+  if (attr < lds) {
+    (void)hipFuncSetAttribute((const void*)decode_gemm_kernel<AMODE, ACT, RMODE, CF32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = lds;
+  }
+  hipLaunchKernelGGL((decode_gemm_kernel<AMODE, ACT, RMODE, CF32>), dim3((unsigned)nblk), dim3(256), lds, s, *g);
+  MIT_LAUNCH_CHECK("mit_decode_gemm");
+  return MIT_OK;
+}
+}  // namespace
+
+extern "C" int mit_decode_gemm(const mit_decode_gemm_args* g, void* stream) {
+  MIT_CHECK_ARG(g != nullptr, "mit_decode_gemm: null args");
+  MIT_RECORD([c = *g, stream]() { return mit_decode_gemm(&c, stream); });
+  MIT_CHECK_ARG(g->M >= 0 && g->N > 0 && g->K > 0, "mit_decode_gemm: bad extents M=%ld N=%ld K=%ld", g->M, g->N, g->K);
+  MIT_CHECK_ARG(g->A && g->B, "mit_decode_gemm: null operand");
+  MIT_CHECK_ARG(g->C || g->z_out, "mit_decode_gemm: no output");
+  MIT_CHECK_ARG(g->K % 8 == 0 && g->N % 8 == 0 && g->ldb % 8 == 0 && g->lda >= g->K && g->ldb >= g->K,
+                "mit_decode_gemm: K, N, ldb must be multiples of 8 and lda/ldb >= K");
+  MIT_CHECK_ARG(g->act == MIT_ACT_NONE || g->act == MIT_ACT_RELU, "mit_decode_gemm: act %d unsupported", g->act);
+  MIT_CHECK_ARG(g->r_mode >= 0 && g->r_mode <= 2, "mit_decode_gemm: bad r_mode %d", g->r_mode);
+  const bool lna = g->a_stats != nullptr;
+  MIT_CHECK_ARG(!lna || (g->a_gamma && g->a_beta && g->K <= 64 * DG_PMAX && g->lda % 4 == 0),
+                "mit_decode_gemm: LN operand needs gamma/beta, K <= 1024, lda % 4 == 0");
+  MIT_CHECK_ARG(lna || g->lda % 8 == 0, "mit_decode_gemm: bf16 A needs lda % 8 == 0");
+  MIT_CHECK_ARG(g->r_mode == 0 || (g->r && g->ldr >= g->N && g->ldr % 8 == 0), "mit_decode_gemm: bad residual");
+  MIT_CHECK_ARG(g->r_mode != 2 || (g->r_stats && g->r_gamma && g->r_beta && g->N <= 64 * DG_PMAX),
+                "mit_decode_gemm: LN residual needs stats and N <= 1024");
+  MIT_CHECK_ARG(!g->C || (g->ldc >= g->N && g->ldc % 8 == 0), "mit_decode_gemm: bad ldc");
+  MIT_CHECK_ARG(!g->z_out || (g->ldz >= g->N && g->ldz % 8 == 0), "mit_decode_gemm: bad ldz");
+  MIT_CHECK_ARG(!g->cache || (g->pos && g->kv_col0 % 8 == 0 && g->c_row % 8 == 0 && g->c_batch % 8 == 0),
+                "mit_decode_gemm: cache needs pos and 8-element aligned strides");
+  MIT_CHECK_ARG(!g->stats_out || g->z_out, "mit_decode_gemm: stats_out needs z_out");
+  MIT_CHECK_ARG(2 * ((g->N - 1) * g->ldb + g->K) < (1L << 31) && (lna || 2 * ((g->M - 1) * g->lda + g->K) < (1L << 31)),
+                "mit_decode_gemm: operand spans >= 2 GiB");
+  const uintptr_t al = (uintptr_t)g->A | (uintptr_t)g->B | (uintptr_t)g->C | (uintptr_t)g->z_out | (uintptr_t)g->r |
+                       (uintptr_t)g->cache | (uintptr_t)g->a_gamma | (uintptr_t)g->a_beta | (uintptr_t)g->r_gamma |
+                       (uintptr_t)g->r_beta;
+  MIT_CHECK_ARG(al % 16 == 0, "mit_decode_gemm: pointers must be 16-B aligned");
+  if (g->M == 0) return MIT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool relu = g->act == MIT_ACT_RELU;
+  if (g->c_f32) {
+    MIT_CHECK_ARG(lna && !relu && g->r_mode == 0, "mit_decode_gemm: f32 C only for the LN-operand head GEMM");
+    return launch_decode_gemm<1, MIT_ACT_NONE, 0, true>(g, s);
+  }
+  if (lna) {
+    MIT_CHECK_ARG(g->r_mode == 0, "mit_decode_gemm: LN operand with a residual unsupported");
+    return relu ? launch_decode_gemm<1, MIT_ACT_RELU, 0, false>(g, s) : launch_decode_gemm<1, MIT_ACT_NONE, 0, false>(g, s);
+  }
+  MIT_CHECK_ARG(!relu || g->r_mode == 0, "mit_decode_gemm: ReLU with a residual unsupported");
+  if (relu) return launch_decode_gemm<0, MIT_ACT_RELU, 0, false>(g, s);
+  switch (g->r_mode) {
+    case 1: return launch_decode_gemm<0, MIT_ACT_NONE, 1, false>(g, s);
+    case 2: return launch_decode_gemm<0, MIT_ACT_NONE, 2, false>(g, s);
+    default: return launch_decode_gemm<0, MIT_ACT_NONE, 0, false>(g, s);
+  }
+}
+
+extern "C" int mit_decode_layernorm(long M, long W, const float* z, long ldz, const float* stats, const float* gamma,
+                                    const float* beta, float eps, void* out, long ldo, void* stream) {
+  MIT_RECORD([=]() { return mit_decode_layernorm(M, W, z, ldz, stats, gamma, beta, eps, out, ldo, stream); });
+  MIT_CHECK_ARG(z && stats && gamma && beta && out, "mit_decode_layernorm: null pointer");
+  MIT_CHECK_ARG(W > 0 && W % 8 == 0 && W <= 64 * DG_PMAX && ldz >= W && ldo >= W && ldz % 4 == 0 && ldo % 8 == 0,
+                "mit_decode_layernorm: bad extents W=%ld ldz=%ld ldo=%ld", W, ldz, ldo);
+  MIT_CHECK_ARG((((uintptr_t)z | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)out) % 16) == 0,
+                "mit_decode_layernorm: pointers must be 16-B aligned");
+  if (M <= 0) return MIT_OK;
+  hipLaunchKernelGGL(decode_ln_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, M, W, z, ldz,
+                     stats, gamma, beta, eps, (bf16*)out, ldo);
+  MIT_LAUNCH_CHECK("mit_decode_layernorm");
   return MIT_OK;
 }

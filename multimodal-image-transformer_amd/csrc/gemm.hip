@@ -1109,12 +1109,16 @@ __global__ void gemm_splitk_reduce(long M, long N, int ksplit, const float* __re
 // split-K plan for a plain-epilogue bf16 GEMM: only when the output has too few 128x128 tiles to
 // fill 256 CUs and K is long (the weight-gradient shapes). Returns 1 (no split) otherwise.
 int g_split_target = -1;  // blocks the split aims for (env MIT_SPLITK_TARGET; 128 beat 512 / 256 / 64 by 0.8-4 % in the step: fewer fp32 slabs)
-int splitk_plan(long M, long N, long K, long* kchunk) {
+int g_split_target_dx = -1;  // the same for K-contig A (data gradients on the main stream; env MIT_SPLITK_TARGET_DX)
+int splitk_plan(long M, long N, long K, long* kchunk, int a_layout = MIT_MN_CONTIG) {
   const long tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   *kchunk = K;
   if (g_split_target < 0) g_split_target = getenv("MIT_SPLITK_TARGET") ? atoi(getenv("MIT_SPLITK_TARGET")) : 128;
+  if (g_split_target_dx < 0)
+    g_split_target_dx = getenv("MIT_SPLITK_TARGET_DX") ? atoi(getenv("MIT_SPLITK_TARGET_DX")) : 256;  // 256 beat 128 by 0.4 % in the step (dX fc_out: K = 10000 on 128 tiles)
   if (tiles >= 256 || K < 1024 || N % 8) return 1;
-  long s = (g_split_target + tiles - 1) / tiles;
+  const long target = a_layout == MIT_K_CONTIG ? g_split_target_dx : 256;  // 256 beat 128 by 0.4 % in the step (dX fc_out: K = 10000 on 128 tiles)
+  long s = (target + tiles - 1) / tiles;
   s = min(s, K / 512);
   s = min(s, 16L);
   if (s < 2) return 1;
@@ -1409,7 +1413,7 @@ Split plan_split(const mit_gemm_args* g) {
   const bool plain = !g->bias && g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f;
   long kc;
   if (plain && g->ldc % 4 == 0 && al16(g->C)) {
-    const int s = splitk_plan(g->M, g->N, g->K, &kc);
+    const int s = splitk_plan(g->M, g->N, g->K, &kc, g->a_layout);
     if (s > 1 && splitk_ws_bytes(g->M, g->N, s) <= g->workspace_bytes) {
       p.ks = s;
       p.kchunk = kc;
@@ -1448,7 +1452,8 @@ extern "C" int mit_gemm_set_fused_split(int on) {
 
 extern "C" long mit_gemm_workspace_bytes(long M, long N, long K) {
   long kc;
-  const long a = splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc));
+  const long a = max(splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc)),
+                     splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc, MIT_K_CONTIG)));
   const long b = fused_ws_bytes(M, N, fused_plan(M, N, K, &kc));
   return a > b ? a : b;
 }

@@ -267,6 +267,14 @@ class DecodeState:
         self.x, self.x1, self.x2, self.y, self.o, self.q = e(d), e(d), e(d), e(d), e(d), e(d)
         self.qkv, self.h = e(3 * d), e(F)
         self.logits = torch.empty(B, padded_vocab(V), dtype=torch.float32, device=dev)  # f32: argmax on unrounded logits
+        # bf16 step with the LayerNorms folded into the GEMMs (native.decode_gemm): the three pre-LN sums
+        # of a layer in f32 and their per-64-column row statistics; the pick advances pos via `ticket`
+        self.fused = dt == torch.bfloat16 and os.environ.get("MIT_DECODE_FUSED", "1") != "0"
+        if self.fused:
+            P = (d + 63) // 64
+            self.z = [torch.empty(B, d, dtype=torch.float32, device=dev) for _ in range(3)]
+            self.zst = [torch.empty(B, P, 2, dtype=torch.float32, device=dev) for _ in range(3)]
+            self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def token_lists(self) -> List[List[int]]:
         """Per row: START .. up to and including the first END (model.py:236-242), else max_len ids."""
@@ -592,6 +600,8 @@ class TransformerDecoder:
     def decode_step(self, stt: "DecodeState"):
         """One greedy token for every row: position p = stt.pos (device) -> ids[:, p+1]; p += 1.
         No host synchronisation: capturable into a hipGraph."""
+        if stt.fused:
+            return self._decode_step_fused(stt)
         d, H, L, V = self.d, self.H, self.L, self.V
         st, w = self.store, self.store.w
         B, S, Tm = stt.B, stt.S, stt.max_len
@@ -604,7 +614,7 @@ class TransformerDecoder:
             native.kv_store(stt.qkv[:, d:], 3 * d, cache, 2 * d, Tm * 2 * d, B, 2 * d, stt.pos)
             native.attention_decode(stt.qkv, 3 * d, cache, 2 * d, Tm * 2 * d, cache[:, :, d:], 2 * d, Tm * 2 * d, stt.o,
                                     d, B, H, pos=stt.pos, key_tokens=stt.ids, tok_batch=Tm, pad_idx=self.pad_idx,
-                                    scale=1.0 / math.sqrt(self.hd))
+                                    scale=1.0 / math.sqrt(self.hd), Dh=self.hd)
             native.linear(stt.o, w(pre + "self_out.weight"), stt.y, bias=st.p(pre + "self_out.bias"))
             native.layernorm_fwd(x, st.p(pre + "norm1.weight"), st.p(pre + "norm1.bias"), 1e-5, stt.x1, r=stt.y)
             native.linear(stt.x1, w(pre + "cross_q.weight"), stt.q, bias=st.p(pre + "cross_q.bias"))
@@ -620,6 +630,52 @@ class TransformerDecoder:
         native.linear(x, w("fc_out.weight"), stt.logits, bias=st.p("fc_out.bias"))
         native.greedy_pick(stt.logits, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished, stt.n_finished, V=V)
         native.step_inc(stt.pos)
+
+    def _decode_step_fused(self, stt: "DecodeState"):
+        """decode_step on bf16 with 8 GEMM/attention launches per layer (was 12): every post-LN residual
+        block (transformer.py:1144-1153) is z = sublayer + LN_prev(z_prev) written in f32 by the
+        GEMM that produces the sublayer output, and LN(z) is applied by its consumers (the next
+        GEMM's operand staging / residual epilogue); the self-attention K|V row goes straight from the
+        in_proj GEMM into the cache; the pick advances the position."""
+        d, H, L, V = self.d, self.H, self.L, self.V
+        st, w, p = self.store, self.store.w, self.store.p
+        B, S, Tm = stt.B, stt.S, stt.max_len
+        z1, z2, z3 = stt.z
+        s1, s2, s3 = stt.zst
+        scale = 1.0 / math.sqrt(self.hd)
+        native.embed_decode(stt.ids, stt.pos, w("token_embedding.weight"), math.sqrt(d), self.pe, stt.x)
+        for l in range(L):
+            pre = f"layers.{l}."
+            cache = stt.cache[l]
+            if l == 0:
+                a, a_ln = stt.x, None
+            else:
+                q3 = f"layers.{l - 1}.norm3."
+                a, a_ln = z3, (s3, p(q3 + "weight"), p(q3 + "bias"))
+            ln1 = (s1, p(pre + "norm1.weight"), p(pre + "norm1.bias"))
+            ln2 = (s2, p(pre + "norm2.weight"), p(pre + "norm2.bias"))
+            native.decode_gemm(a, w(pre + "self_in.weight"), out=stt.qkv, bias=p(pre + "self_in.bias"), a_ln=a_ln,
+                               cache=cache, c_row=2 * d, c_batch=Tm * 2 * d, kv_col0=d, pos=stt.pos)
+            native.attention_decode(stt.qkv, 3 * d, cache, 2 * d, Tm * 2 * d, cache[:, :, d:], 2 * d, Tm * 2 * d, stt.o,
+                                    d, B, H, pos=stt.pos, key_tokens=stt.ids, tok_batch=Tm, pad_idx=self.pad_idx,
+                                    scale=scale, Dh=self.hd)
+            native.decode_gemm(stt.o, w(pre + "self_out.weight"), bias=p(pre + "self_out.bias"), residual=a, r_ln=a_ln,
+                               z_out=z1, stats_out=s1)
+            native.decode_gemm(z1, w(pre + "cross_q.weight"), out=stt.q, bias=p(pre + "cross_q.bias"), a_ln=ln1)
+            kvl = stt.kv[l]
+            native.attention_decode(stt.q, d, kvl, 2 * d, S * 2 * d, kvl[:, d:], 2 * d, S * 2 * d,
+                                    stt.o, d, B, H, Lk=S, scale=scale, Dh=self.hd)
+            native.decode_gemm(stt.o, w(pre + "cross_out.weight"), bias=p(pre + "cross_out.bias"), residual=z1,
+                               r_ln=ln1, z_out=z2, stats_out=s2)
+            native.decode_gemm(z2, w(pre + "linear1.weight"), out=stt.h, bias=p(pre + "linear1.bias"),
+                               act=native.ACT_RELU, a_ln=ln2)
+            native.decode_gemm(stt.h, w(pre + "linear2.weight"), bias=p(pre + "linear2.bias"), residual=z2, r_ln=ln2,
+                               z_out=z3, stats_out=s3)
+        q3 = f"layers.{L - 1}.norm3."
+        native.decode_layernorm(z3, s3, p(q3 + "weight"), p(q3 + "bias"), stt.x)
+        native.linear(stt.x, w("fc_out.weight"), stt.logits, bias=p("fc_out.bias"))
+        native.greedy_pick_advance(stt.logits, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished,
+                                   stt.n_finished, stt.ticket, V=V)
 
     def forward(self, tgt_tokens: torch.Tensor, memory: torch.Tensor, memory_padding_mask=None) -> torch.Tensor:
         """decoder.py:134-193: f32 logits [B, T, V] (no autograd; training goes through the model's

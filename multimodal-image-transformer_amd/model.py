@@ -461,12 +461,18 @@ class ImageToTextModel:
 
     @torch.no_grad()
     def generate_batch(self, images, start_token_id: int, end_token_id: int, max_len: int = 100,
-                       use_graph: bool = True, check_every: int = 8) -> List[List[int]]:
+                       use_graph: bool = True, check_every: int = 8, streams: Optional[int] = None) -> List[List[int]]:
         """Greedy captions for a whole batch (BASELINE config 5): per image the same token list as
         generate() (model.py:171-242: START, argmax of the last position each step, stop after END,
         at most max_len ids), computed with cached self-attention K/V, the cross-attention K/V of
         the image memory computed once, and ONE hipGraph-captured step replayed per token. The host
-        checks the finished count every `check_every` tokens (the only synchronisation)."""
+        checks the finished count every `check_every` tokens (the only synchronisation).
+
+        streams: the images are decoded as this many independent row groups, each with its own state
+        and graph, replayed on its own HIP stream so the groups' latency-bound launches overlap
+        (default: env MIT_DECODE_STREAMS, else 4 groups of >= 32 images). Rows never interact in
+        greedy decoding and every kernel computes a row the same way at any batch size, so the ids
+        do not depend on the grouping."""
         self.eval()
         pv = images if isinstance(images, torch.Tensor) else \
             self.image_processor(images=images, return_tensors="pt")["pixel_values"]
@@ -474,27 +480,45 @@ class ImageToTextModel:
         B = pv.shape[0]
         mem, mem_ld, S, _, _ = self._encode_memory(pv)
         dec = self.decoder
-        stt = dec.decode_begin(mem, mem_ld, S, B, max_len, start_token_id, end_token_id)
+        if streams is None:
+            streams = int(os.environ.get("MIT_DECODE_STREAMS", "0")) or max(1, min(4, B // 32))
+        G = max(1, min(int(streams), B))
+        bounds = [B * i // G for i in range(G + 1)]
+        states = [dec.decode_begin(mem[bounds[i] * S:bounds[i + 1] * S], mem_ld, S, bounds[i + 1] - bounds[i], max_len,
+                                   start_token_id, end_token_id) for i in range(G)]
         steps = max_len - 1
-        if steps <= 0:
-            return stt.token_lists()
-        dec.decode_step(stt)  # position 0 (eager: warms every kernel before capture)
-        done = 1
-        if use_graph and steps > 1:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                dec.decode_step(stt)
-            run = graph.replay
-        else:
-            run = lambda: dec.decode_step(stt)  # noqa: E731
-        while done < steps:
-            n = min(check_every, steps - done)
-            for _ in range(n):
-                run()
-            done += n
-            if int(stt.n_finished.item()) == B:
-                break
-        return stt.token_lists()
+        if steps > 0:
+            for stt in states:
+                dec.decode_step(stt)  # position 0 (eager: warms every kernel before capture)
+            done = 1
+            cur = torch.cuda.current_stream()
+            side = [cur] + [torch.cuda.Stream(device=self.device) for _ in range(G - 1)]
+            if use_graph and steps > 1:
+                runs = []
+                for stt in states:
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph):
+                        dec.decode_step(stt)
+                    runs.append(graph.replay)
+            else:
+                runs = [(lambda s_=stt: dec.decode_step(s_)) for stt in states]
+            for s_ in side[1:]:
+                s_.wait_stream(cur)
+            while done < steps:
+                n = min(check_every, steps - done)
+                for _ in range(n):
+                    for run, s_ in zip(runs, side):
+                        with torch.cuda.stream(s_):
+                            run()
+                done += n
+                if sum(int(stt.n_finished.item()) for stt in states) == B:
+                    break
+            for s_ in side[1:]:
+                cur.wait_stream(s_)
+        out = []
+        for stt in states:
+            out.extend(stt.token_lists())
+        return out
 
     # --- checkpoints (reference key names) --------------------------------------
     def state_dict(self) -> Dict[str, torch.Tensor]:

@@ -44,6 +44,14 @@ class GemmArgs(ctypes.Structure):
                 ("accumulate", I), ("rowsum", vp), ("workspace", vp), ("workspace_bytes", L)]
 
 
+class DecodeGemmArgs(ctypes.Structure):
+    _fields_ = [("M", L), ("N", L), ("K", L), ("A", vp), ("lda", L), ("a_stats", vp), ("a_gamma", vp),
+                ("a_beta", vp), ("B", vp), ("ldb", L), ("bias", vp), ("act", I), ("c_f32", I), ("C", vp),
+                ("ldc", L), ("r_mode", I), ("r", vp), ("ldr", L), ("r_stats", vp), ("r_gamma", vp),
+                ("r_beta", vp), ("eps", Fl), ("z_out", vp), ("ldz", L), ("stats_out", vp), ("cache", vp),
+                ("c_row", L), ("c_batch", L), ("kv_col0", L), ("pos", vp)]
+
+
 class AttnArgs(ctypes.Structure):
     _fields_ = [("q", vp), ("q_row", L), ("q_batch", L), ("k", vp), ("k_row", L), ("k_batch", L),
                 ("v", vp), ("v_row", L), ("v_batch", L), ("o", vp), ("o_row", L), ("o_batch", L),
@@ -103,6 +111,9 @@ SIGNATURES = {
     "mit_event_record": (I, [vp, vp]),
     "mit_stream_wait_event": (I, [vp, vp]),
     "mit_greedy_pick": (I, [L, L, vp, L, vp, L, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp]),
+    "mit_greedy_pick_advance": (I, [L, L, vp, L, vp, L, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp]),
+    "mit_decode_gemm": (I, [ctypes.POINTER(DecodeGemmArgs), vp]),
+    "mit_decode_layernorm": (I, [L, L, vp, L, vp, vp, vp, Fl, vp, L, vp]),
 }
 
 
@@ -540,6 +551,43 @@ def greedy_pick(logits, ids, pos, end_id, pad_id, finished, n_finished, V=None):
     V = V if V is not None else logits.shape[1]
     _check(lib().mit_greedy_pick(B, V, ptr(logits), logits.stride(0), ptr(ids), ids.shape[1], ptr(pos), int(end_id),
                                  int(pad_id), ptr(finished), ptr(n_finished), stream_ptr()), "mit_greedy_pick")
+
+
+def greedy_pick_advance(logits, ids, pos, end_id, pad_id, finished, n_finished, ticket, V=None):
+    """greedy_pick, then pos += 1 (int32 `ticket` device counter, 0 before and after)."""
+    B = logits.shape[0]
+    V = V if V is not None else logits.shape[1]
+    _check(lib().mit_greedy_pick_advance(B, V, ptr(logits), logits.stride(0), ptr(ids), ids.shape[1], ptr(pos),
+                                         int(end_id), int(pad_id), ptr(finished), ptr(n_finished), ptr(ticket),
+                                         stream_ptr()), "mit_greedy_pick_advance")
+
+
+def decode_gemm(a, w, *, out=None, bias=None, act=ACT_NONE, a_ln=None, residual=None, r_ln=None, eps=1e-5,
+                z_out=None, stats_out=None, cache=None, c_row=0, c_batch=0, kv_col0=0, pos=None):
+    """Decode-step GEMM (mit_decode_gemm): out = act(A' w^T + bias) (+ residual), w bf16 [N, K].
+    a: bf16 rows [M, K], or f32 pre-LN sums when a_ln = (stats, gamma, beta) (A' = LN(a));
+    residual: bf16 rows, or f32 pre-LN sums when r_ln = (stats, gamma, beta) (+ LN(residual));
+    z_out / stats_out: f32 pre-LN sum of the next LayerNorm and its per-64-column row statistics
+    [M, ceil(N/64), 2]; cache: the columns >= kv_col0 also go to cache[m*c_batch + pos*c_row + n - kv_col0]."""
+    M, K = a.shape[0], a.shape[-1]
+    N = w.shape[0]
+    r_mode = 0 if residual is None else (2 if r_ln is not None else 1)
+    g = DecodeGemmArgs(M, N, K, ptr(a), a.stride(0), ptr(a_ln[0]) if a_ln else None, ptr(a_ln[1]) if a_ln else None,
+                       ptr(a_ln[2]) if a_ln else None, ptr(w), w.stride(0), ptr(bias), act,
+                       1 if out is not None and out.dtype == torch.float32 else 0, ptr(out),
+                       out.stride(0) if out is not None else 0, r_mode, ptr(residual),
+                       residual.stride(0) if residual is not None else 0, ptr(r_ln[0]) if r_ln else None,
+                       ptr(r_ln[1]) if r_ln else None, ptr(r_ln[2]) if r_ln else None, eps, ptr(z_out),
+                       z_out.stride(0) if z_out is not None else 0, ptr(stats_out), ptr(cache), c_row, c_batch, kv_col0,
+                       ptr(pos))
+    _check(lib().mit_decode_gemm(ctypes.byref(g), stream_ptr()), "mit_decode_gemm")
+
+
+def decode_layernorm(z, stats, gamma, beta, out, eps=1e-5):
+    """out (bf16 [M, W]) = LN(z) from mit_decode_gemm row statistics."""
+    M, W = z.shape
+    _check(lib().mit_decode_layernorm(M, W, ptr(z), z.stride(0), ptr(stats), ptr(gamma), ptr(beta), eps, ptr(out),
+                                      out.stride(0), stream_ptr()), "mit_decode_layernorm")
 
 
 def image_normalize(src_u8, dst, mean, std):

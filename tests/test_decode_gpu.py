@@ -228,3 +228,162 @@ def test_generate_batch_b256_bf16_agrees_with_full_forward():
     print(f"b256 bf16 decode: {tied} rows stopped at a near-tie, {bad} real disagreements")
     assert bad == 0
     assert tied <= 256 // 4
+
+
+# --- fused bf16 decode step (mit_decode_gemm, mit_greedy_pick_advance) ---------------------------
+def _ln_ref(z, gamma, beta, eps=1e-5):
+    z = z.double()
+    mu = z.mean(-1, keepdim=True)
+    var = z.var(-1, unbiased=False, keepdim=True)
+    return (z - mu) / torch.sqrt(var + eps) * gamma.double() + beta.double()
+
+
+def _stats(z, dev):
+    """(mean, M2) per row over each 64-column tile -- the producer-side statistics mit_decode_gemm writes."""
+    M, W = z.shape
+    P = (W + 63) // 64
+    out = torch.empty(M, P, 2, dtype=torch.float32)
+    for p in range(P):
+        t = z[:, 64 * p:64 * p + 64].double()
+        mu = t.mean(-1)
+        out[:, p, 0] = mu.float()
+        out[:, p, 1] = ((t - mu[:, None]) ** 2).sum(-1).float()
+    return out.to(dev)
+
+
+@pytest.mark.parametrize("M,Nc,K", [(256, 512, 512), (3, 1024, 512), (70, 192, 192), (256, 512, 2048), (5, 136, 128)])
+def test_decode_gemm_residual_ln_chain(M, Nc, K):
+    """z_out = A W^T + b + LN(r) and its per-tile row statistics, then a consumer GEMM on LN(z_out)
+    (operand staging) and one with a bf16 residual and ReLU; float64 references."""
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(M * 7 + Nc + K)
+    a = (torch.randn(M, K, generator=g)).to(dev, torch.bfloat16)
+    w = (torch.randn(Nc, K, generator=g) / K ** 0.5).to(dev, torch.bfloat16)
+    bias = torch.randn(Nc, generator=g).to(dev)
+    r = (torch.randn(M, Nc, generator=g) * 2 + 0.5).to(dev)
+    gr, br = (1 + 0.1 * torch.randn(Nc, generator=g)).to(dev), (0.1 * torch.randn(Nc, generator=g)).to(dev)
+    r_st = _stats(r.cpu(), dev)
+    z = torch.empty(M, Nc, device=dev)
+    P = (Nc + 63) // 64
+    st = torch.full((M, P, 2), float("nan"), device=dev)
+    N.decode_gemm(a, w, bias=bias, residual=r, r_ln=(r_st, gr, br), z_out=z, stats_out=st)
+    ref = a.double().cpu() @ w.double().cpu().t() + bias.double().cpu() + _ln_ref(r.cpu(), gr.cpu(), br.cpu())
+    assert (z.double().cpu() - ref).abs().max().item() < 2e-3 * ref.abs().max().item()
+    want = _stats(z.cpu(), "cpu")
+    assert torch.allclose(st.cpu(), want, rtol=1e-4, atol=1e-3)
+    if Nc <= 1024:  # materialised LN(z) (the vocabulary head's operand)
+        ln = torch.empty(M, Nc, device=dev, dtype=torch.bfloat16)
+        N.decode_layernorm(z, st, gr, br, ln)
+        want_ln = _ln_ref(z.cpu(), gr.cpu(), br.cpu())
+        assert (ln.double().cpu() - want_ln).abs().max().item() < 2e-2 * want_ln.abs().max().item()
+    # consumer: LN(z) as the A operand
+    N2 = 3 * 64 + 8
+    w2 = (torch.randn(N2, Nc, generator=g) / Nc ** 0.5).to(dev, torch.bfloat16)
+    g2, b2 = (1 + 0.1 * torch.randn(Nc, generator=g)).to(dev), (0.1 * torch.randn(Nc, generator=g)).to(dev)
+    out = torch.empty(M, N2, device=dev, dtype=torch.bfloat16)
+    if Nc <= 1024:
+        N.decode_gemm(z, w2, out=out, act=N.ACT_RELU, a_ln=(st, g2, b2))
+        x = _ln_ref(z.cpu(), g2.cpu(), b2.cpu())
+        ref2 = torch.relu(x @ w2.double().cpu().t())
+        err = (out.double().cpu() - ref2).abs().max().item()
+        assert err < 3e-2 * max(1.0, ref2.abs().max().item()), err
+    # bf16 residual, f32 head output
+    x16 = torch.randn(M, Nc, generator=g).to(dev, torch.bfloat16)
+    z2 = torch.empty(M, Nc, device=dev)
+    st2 = torch.empty(M, P, 2, device=dev)
+    N.decode_gemm(a, w, residual=x16, z_out=z2, stats_out=st2)
+    ref3 = a.double().cpu() @ w.double().cpu().t() + x16.double().cpu()
+    assert (z2.double().cpu() - ref3).abs().max().item() < 2e-3 * ref3.abs().max().item()
+    if Nc <= 1024:
+        logits = torch.empty(M, N2, device=dev)
+        N.decode_gemm(z2, w2, out=logits, bias=torch.zeros(N2, device=dev), a_ln=(st2, g2, b2))
+        ref4 = _ln_ref(z2.cpu(), g2.cpu(), b2.cpu()) @ w2.double().cpu().t()
+        assert (logits.double().cpu() - ref4).abs().max().item() < 3e-2 * max(1.0, ref4.abs().max().item())
+
+
+def test_decode_gemm_writes_kv_cache_row():
+    """The in_proj GEMM's K|V columns land in cache[b, pos, :] (what mit_kv_store did), the rest untouched."""
+    dev = torch.device("cuda")
+    B, d, Tm = 7, 128, 9
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(B, d, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(3 * d, d, generator=g) / d ** 0.5).to(dev, torch.bfloat16)
+    qkv = torch.empty(B, 3 * d, device=dev, dtype=torch.bfloat16)
+    cache = torch.zeros(B, Tm, 2 * d, device=dev, dtype=torch.bfloat16)
+    pos = torch.tensor([4], dtype=torch.int64, device=dev)
+    N.decode_gemm(a, w, out=qkv, cache=cache, c_row=2 * d, c_batch=Tm * 2 * d, kv_col0=d, pos=pos)
+    c = cache.cpu()
+    assert torch.equal(c[:, 4], qkv[:, d:].cpu())
+    c[:, 4] = 0
+    assert not c.any()
+
+
+def test_decode_gemm_rejects_bad_args():
+    dev = torch.device("cuda")
+    a = torch.zeros(4, 12, device=dev, dtype=torch.bfloat16)  # K % 8 != 0
+    w = torch.zeros(16, 12, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(N.NativeError):
+        N.decode_gemm(a, w, out=torch.empty(4, 16, device=dev, dtype=torch.bfloat16))
+    a = torch.zeros(4, 16, device=dev, dtype=torch.bfloat16)
+    w = torch.zeros(16, 16, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(N.NativeError):  # no output at all
+        N.decode_gemm(a, w)
+    with pytest.raises(N.NativeError):  # stats without z_out
+        N.decode_gemm(a, w, out=torch.empty(4, 16, device=dev, dtype=torch.bfloat16),
+                      stats_out=torch.empty(4, 1, 2, device=dev))
+
+
+def test_greedy_pick_advance_moves_pos_once():
+    dev = torch.device("cuda")
+    B, V, T = 300, 777, 8
+    logits = torch.randn(B, V, device=dev)
+    ids = torch.zeros(B, T, dtype=torch.int64, device=dev)
+    ids2 = ids.clone()
+    pos = torch.tensor([2], dtype=torch.int64, device=dev)
+    fin, nf = torch.zeros(B, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)
+    fin2, nf2 = fin.clone(), nf.clone()
+    ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+    N.greedy_pick(logits, ids2, pos, 5, 0, fin2, nf2)
+    for step in range(3):
+        N.greedy_pick_advance(logits, ids, pos, 5, 0, fin, nf, ticket)
+        assert pos.item() == 3 + step and ticket.item() == 0
+    assert torch.equal(ids[:, 3], ids2[:, 3]) and torch.equal(ids[:, 4], ids2[:, 3])
+
+
+@pytest.mark.parametrize("name", ["tiny_vit_patches", "cfg0_b4_patches"])
+def test_fused_decode_step_matches_unfused(name, monkeypatch):
+    """bf16: the fused step (LayerNorms folded into the GEMMs) and the 12-launch-per-layer step give the
+    same logits up to bf16 rounding of the LN outputs, token after token on a shared prefix."""
+    meta, _ = FX.load(name)
+    m, _ = build_model(meta, torch.bfloat16)
+    m.eval()
+    img = FX.inputs(meta, 0)[0].cuda()
+    imgs = torch.cat([img, img.flip(-1), img * 0.5], 0)
+    mem, mem_ld, S, _, _ = m._encode_memory(imgs.float())
+    dec = m.decoder
+    monkeypatch.setenv("MIT_DECODE_FUSED", "1")
+    a = dec.decode_begin(mem, mem_ld, S, 3, 12, 2, 10 ** 6)
+    monkeypatch.setenv("MIT_DECODE_FUSED", "0")
+    b = dec.decode_begin(mem, mem_ld, S, 3, 12, 2, 10 ** 6)
+    assert a.fused and not b.fused
+    for t in range(8):
+        dec.decode_step(a)
+        dec.decode_step(b)
+        la, lb = a.logits[:, :dec.V].float(), b.logits[:, :dec.V].float()
+        rel = ((la - lb).norm() / lb.norm()).item()
+        assert rel < 1.5e-2, (t, rel)
+        assert a.pos.item() == b.pos.item() == t + 1
+        b.ids.copy_(a.ids)  # share the prefix (near-ties may pick differently)
+
+
+@pytest.mark.parametrize("name,dtype", [("tiny_vit_patches", torch.bfloat16), ("tiny_vit_cls", torch.float32)])
+def test_generate_batch_row_groups_on_streams_equal_one_group(name, dtype):
+    """generate_batch(streams=G): row groups with their own states / graphs on parallel streams give
+    exactly the single-group ids (rows never interact; per-row arithmetic is batch-size independent)."""
+    meta, _ = FX.load(name)
+    m, _ = build_model(meta, dtype)
+    img = FX.inputs(meta, 0)[0]
+    imgs = torch.cat([img, img.flip(-1), img * 0.5, img.flip(-2), -img], 0).cuda()
+    one = m.generate_batch(imgs, 2, 10 ** 6, max_len=14, streams=1)
+    for G in (2, 3, 5):
+        assert m.generate_batch(imgs, 2, 10 ** 6, max_len=14, streams=G) == one, G
