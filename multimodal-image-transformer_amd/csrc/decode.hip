@@ -136,6 +136,83 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(long H, const T* __res
   }
 }
 
+// The same decode attention for d_model = H * DH = 512 with one 8-wave block per IMAGE: a wave
+// instruction reads one whole 1-KiB key (or value) row -- lane l holds dims 8l .. 8l+7, i.e. head
+// 8l / DH, and a head's score is reduced over its DH / 8 lanes -- so a block streams its image's K/V
+// rows contiguously (the (b, h)-block kernel reads 128-B pieces of every row, 8 times per DRAM page)
+// with U rows per wave in flight before the first use. Wave w takes keys w*U .. w*U+U-1 (+8U per
+// iteration); the 8 waves' softmax states merge once in LDS.
+template <int DH, int U>
+__global__ __launch_bounds__(512) void attn_decode_rows_kernel(const bf16* __restrict__ q, long q_batch,
+                                                               const bf16* __restrict__ k, long k_row, long k_batch,
+                                                               const bf16* __restrict__ v, long v_row, long v_batch,
+                                                               bf16* __restrict__ o, long o_batch, long lk_fixed,
+                                                               const int64_t* __restrict__ pos,
+                                                               const int64_t* __restrict__ key_tokens, long tok_batch,
+                                                               int pad_idx, float scale) {
+  constexpr int LPH = DH / 8;
+  __shared__ float red[8][64][10];
+  const long b = blockIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const long Lk = pos ? (*pos + 1) : lk_fixed;
+  float qv[8];
+  load8<bf16>(q + b * q_batch + lane * 8, qv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) qv[i] *= scale * kLog2e;
+  const bf16* kb = k + b * k_batch + lane * 8;
+  const bf16* vb = v + b * v_batch + lane * 8;
+  const int64_t* tb = key_tokens ? key_tokens + b * tok_batch : nullptr;
+  float m = kNegBig, l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (long j0 = (long)w * U; j0 < Lk; j0 += 8 * U) {
+    bf16x8 kr[U], vr[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long j = j0 + u;
+      ok[u] = j < Lk;
+      if (ok[u]) {
+        kr[u] = *(const bf16x8*)(kb + j * k_row);
+        vr[u] = *(const bf16x8*)(vb + j * v_row);
+      } else {
+        kr[u] = vr[u] = bf16x8{};
+      }
+    }
+    if (tb) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) ok[u] = ok[u] && tb[j0 + u] != pad_idx;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s = fmaf(qv[i], (float)kr[u][i], s);
+#pragma unroll
+      for (int x = 1; x < LPH; x <<= 1) s += __shfl_xor(s, x, 64);
+      if (!ok[u]) s = -INFINITY;
+      const float mn = fmaxf(m, s);
+      const float corr = exp2f(m - mn), p = exp2f(s - mn);
+      l = l * corr + p;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(p, (float)vr[u][i], acc[i] * corr);
+      m = mn;
+    }
+  }
+  float* mine = red[w][lane];
+  mine[0] = m;
+  mine[1] = l;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mine[2 + i] = acc[i];
+  __syncthreads();
+  if (w == 0) {
+    for (int w2 = 1; w2 < 8; ++w2) merge(m, l, acc, red[w2][lane][0], red[w2][lane][1], &red[w2][lane][2]);
+    float out[8];
+    const float inv = 1.0f / l;  // all keys masked -> 0/0 = NaN, as the reference's softmax
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = acc[i] * inv;
+    store8<bf16>(o + b * o_batch + lane * 8, out);
+  }
+}
+
 template <typename T>
 __global__ void kv_store_kernel(long B, long n, const T* __restrict__ src, long s_batch, T* __restrict__ cache,
                                 long c_row, long c_batch, const int64_t* __restrict__ pos) {
@@ -243,7 +320,6 @@ __global__ __launch_bounds__(256) void greedy_pick_kernel(long V, const float* _
 // ------------------------------------------------------------------------------------------------
 constexpr int DG_BK = 64;
 constexpr int DG_RLD = 68;                          // fp32 row stride of a partial tile in LDS
-constexpr int DG_RED = 4 * 64 * DG_RLD * 4;         // 69632 B
 constexpr uint32_t DG_OOB = 0x80000000u;
 
 __device__ __forceinline__ int dg_xcd_remap(int bid, int nwg) {
@@ -272,15 +348,20 @@ __device__ __forceinline__ void dg_row_stats(const float* __restrict__ st, long 
   rstd = rsqrtf(m2 / (float)W + eps);
 }
 
-template <int AMODE, int ACT, int RMODE, bool CF32>
-__global__ __launch_bounds__(256) void decode_gemm_kernel(mit_decode_gemm_args g) {
+// NW waves split K; BMR x 64 output tile (BMR = 64, or 32 with 8 waves: half the fragment and
+// accumulator registers, so two buffers of operands still fit 2 waves per SIMD)
+template <int AMODE, int ACT, int RMODE, bool CF32, int NW, int BMR>
+__global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(mit_decode_gemm_args g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int FR = BMR / 16;                          // 16-row fragments per wave
+  constexpr int TPR = 256 / BMR, CPT = 64 / TPR;        // epilogue (threads 0-255): threads per row, columns each
   const long M = g.M, N = g.N, K = g.K;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nbn = (int)((N + 63) / 64), nbm = (int)((M + 63) / 64);
+  const int nbn = (int)((N + 63) / 64), nbm = (int)((M + BMR - 1) / BMR);
   const int bid = dg_xcd_remap(blockIdx.x, nbm * nbn);  // an XCD's blocks: consecutive column blocks of a row block
   const int bm = bid / nbn, bn = bid % nbn;
-  const long m0 = (long)bm * 64, n0 = (long)bn * 64;
+  const long m0 = (long)bm * BMR, n0 = (long)bn * 64;
+  const bool epi = tid < 256;
   const int b_bytes = (int)(2 * ((N - 1) * g.ldb + K));
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, b_bytes, 0x00020000);
   const long brow = n0 + (lane & 15);
@@ -301,6 +382,50 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(mit_decode_gemm_args g
   int s = w;
   if (s < ns) loadb(s, b0);
 
+  // epilogue operands first: none of them depends on the product, so their round trips overlap the
+  // K loop instead of following it
+  const int r = (tid & 255) / TPR, cq = (tid % TPR) * CPT;
+  const long gr = m0 + r;
+  const bool rok = epi && gr < M;
+  float bias[CPT], res[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) bias[c] = res[c] = 0.f;
+  if (g.bias && epi) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) bias[c] = n0 + cq + c < N ? g.bias[n0 + cq + c] : 0.f;
+  }
+  if constexpr (RMODE == 1) {
+    if (rok) {
+#pragma unroll
+      for (int h = 0; h < CPT; h += 8)
+        if (n0 + cq + h < N) {
+          const bf16x8 x = *(const bf16x8*)((const bf16*)g.r + gr * g.ldr + n0 + cq + h);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) res[h + i] = (float)x[i];
+        }
+    }
+  } else if constexpr (RMODE == 2) {
+    if (rok) {
+      const float* zr = (const float*)g.r + gr * g.ldr;
+      f32x4 z[CPT / 4], ga[CPT / 4], be[CPT / 4];
+#pragma unroll
+      for (int c = 0; c < CPT; c += 4) {
+        const long gc = n0 + cq + c;
+        const bool ok = gc < N;
+        z[c / 4] = ok ? *(const f32x4*)(zr + gc) : f32x4{};
+        ga[c / 4] = ok ? *(const f32x4*)(g.r_gamma + gc) : f32x4{};
+        be[c / 4] = ok ? *(const f32x4*)(g.r_beta + gc) : f32x4{};
+      }
+      float mu, rs;
+      dg_row_stats(g.r_stats + gr * 2 * ((N + 63) / 64), N, g.eps, mu, rs);
+#pragma unroll
+      for (int c = 0; c < CPT; c += 4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) res[c + i] = (z[c / 4][i] - mu) * rs * ga[c / 4][i] + be[c / 4][i];
+    }
+  }
+  const long p = g.cache ? *g.pos : 0;
+
   // A operand: bf16 rows straight from global (AMODE 0), or LN(z) rows staged in LDS (AMODE 1)
   const long alda = AMODE ? (K * 2 + 16) : 0;  // LDS row stride (bytes): 16-B pad -> conflict-free reads
   __amdgpu_buffer_rsrc_t ra;
@@ -308,55 +433,50 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(mit_decode_gemm_args g
     const int a_bytes = (int)(2 * ((M - 1) * g.lda + K));
     ra = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, a_bytes, 0x00020000);
   } else {
-    float* st = (float*)(smem + 64 * alda);  // (mean, rstd) of the block's 64 rows
-    if (tid < 64) {
-      float mu = 0.f, rs = 0.f;
-      if (m0 + tid < M) dg_row_stats(g.a_stats + (m0 + tid) * 2 * ((K + 63) / 64), K, g.eps, mu, rs);
-      st[2 * tid] = mu;
-      st[2 * tid + 1] = rs;
-    }
-    __syncthreads();
-    // wave w normalises rows 16w .. 16w+15; lane l owns columns 8l .. 8l+7 (+512 per pass): one
-    // wave instruction reads 2 KiB of a row, and 8 rows' loads are in flight before the first store
-    for (long k = 8L * lane; k < K; k += 512) {
-      const f32x4 g0 = *(const f32x4*)(g.a_gamma + k), g1 = *(const f32x4*)(g.a_gamma + k + 4);
-      const f32x4 e0 = *(const f32x4*)(g.a_beta + k), e1 = *(const f32x4*)(g.a_beta + k + 4);
+    static_assert(NW == 4 && BMR == 64, "LN-operand staging: 4 waves, 64 rows");
+    // wave w normalises rows 16w .. 16w+15; lane l owns columns 8l .. 8l+7 (+512 per pass). The
+    // first pass's z loads go out before the row statistics are merged (lanes 0-15 of the wave,
+    // one row each, shared by shuffles): one round trip, not two
+    float mu_l = 0.f, rs_l = 0.f;
+    if (lane < 16 && m0 + w * 16 + lane < M)
+      dg_row_stats(g.a_stats + (m0 + w * 16 + lane) * 2 * ((K + 63) / 64), K, g.eps, mu_l, rs_l);
+    for (long k = 8L * lane; k - 8L * lane < K; k += 512) {
+      const bool kok = k < K;
+      f32x4 z[16][2];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        f32x4 z[8][2];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = w * 16 + half * 8 + i;
-          if (m0 + r < M) {
-            const float* zr = (const float*)g.A + (m0 + r) * g.lda + k;
-            z[i][0] = *(const f32x4*)zr;
-            z[i][1] = *(const f32x4*)(zr + 4);
-          } else {
-            z[i][0] = z[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
+      for (int i = 0; i < 16; ++i) {
+        const int rr = w * 16 + i;
+        if (kok && m0 + rr < M) {
+          const float* zr = (const float*)g.A + (m0 + rr) * g.lda + k;
+          z[i][0] = *(const f32x4*)zr;
+          z[i][1] = *(const f32x4*)(zr + 4);
+        } else {
+          z[i][0] = z[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+      }
+      const f32x4 g0 = kok ? *(const f32x4*)(g.a_gamma + k) : f32x4{}, g1 = kok ? *(const f32x4*)(g.a_gamma + k + 4) : f32x4{};
+      const f32x4 e0 = kok ? *(const f32x4*)(g.a_beta + k) : f32x4{}, e1 = kok ? *(const f32x4*)(g.a_beta + k + 4) : f32x4{};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = w * 16 + half * 8 + i;
-          const float mu = st[2 * r], rs = st[2 * r + 1];
-          bf16x8 o;
+      for (int i = 0; i < 16; ++i) {
+        const int rr = w * 16 + i;
+        const float mu = __shfl(mu_l, i, 64), rs = __shfl(rs_l, i, 64);
+        bf16x8 o;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            o[j] = (bf16)((z[i][0][j] - mu) * rs * g0[j] + e0[j]);
-            o[j + 4] = (bf16)((z[i][1][j] - mu) * rs * g1[j] + e1[j]);
-          }
-          *(bf16x8*)(smem + r * alda + k * 2) = o;
+        for (int j = 0; j < 4; ++j) {
+          o[j] = (bf16)((z[i][0][j] - mu) * rs * g0[j] + e0[j]);
+          o[j + 4] = (bf16)((z[i][1][j] - mu) * rs * g1[j] + e1[j]);
         }
+        if (kok) *(bf16x8*)(smem + rr * alda + k * 2) = o;
       }
     }
     __syncthreads();
   }
-  auto loada = [&](int s, bf16x8 (&a)[4][2]) {
+  auto loada = [&](int s, bf16x8 (&a)[FR][2]) {
     const long k0 = (long)s * DG_BK + kl;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < FR; ++i) {
         const long k = k0 + kk * 32;
         if constexpr (AMODE == 0) {
           const long row = m0 + i * 16 + (lane & 15);
@@ -369,32 +489,32 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(mit_decode_gemm_args g
       }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[FR][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FR; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](bf16x8 (&a)[4][2], bf16x8 (&b)[4][2]) {
+  auto mma = [&](bf16x8 (&a)[FR][2], bf16x8 (&b)[4][2]) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
   };
-  {  // both operands one K-step ahead of the MFMAs (wave w: K-steps w, w+4, ...)
-    bf16x8 a0[4][2], a1[4][2];
+  {  // both operands one K-step ahead of the MFMAs (wave w: K-steps w, w+NW, ...)
+    bf16x8 a0[FR][2], a1[FR][2];
     if (s < ns) loada(s, a0);
-    for (; s < ns; s += 8) {
-      if (s + 4 < ns) {
-        loada(s + 4, a1);
-        loadb(s + 4, b1);
+    for (; s < ns; s += 2 * NW) {
+      if (s + NW < ns) {
+        loada(s + NW, a1);
+        loadb(s + NW, b1);
       }
       mma(a0, b0);
-      if (s + 4 >= ns) break;
-      if (s + 8 < ns) {
-        loada(s + 8, a0);
-        loadb(s + 8, b0);
+      if (s + NW >= ns) break;
+      if (s + 2 * NW < ns) {
+        loada(s + 2 * NW, a0);
+        loadb(s + 2 * NW, b0);
       }
       mma(a1, b1);
     }
@@ -403,61 +523,23 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(mit_decode_gemm_args g
 
   float* red = (float*)smem;
   {
-    float* mine = red + w * 64 * DG_RLD;
+    float* mine = red + w * BMR * DG_RLD;
     const int gq = lane >> 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FR; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int t = 0; t < 4; ++t) mine[(i * 16 + gq * 4 + t) * DG_RLD + j * 16 + (lane & 15)] = acc[i][j][t];
   }
-  const int r = tid >> 2, cq = (tid & 3) * 16;
-  const long gr = m0 + r;
-  const bool rok = gr < M;
-  // epilogue operands before the barrier
-  float bias[16], res[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) bias[c] = res[c] = 0.f;
-  if (g.bias) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c) bias[c] = n0 + cq + c < N ? g.bias[n0 + cq + c] : 0.f;
-  }
-  if constexpr (RMODE == 1) {
-    if (rok) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if (n0 + cq + 8 * h < N) {
-          const bf16x8 x = *(const bf16x8*)((const bf16*)g.r + gr * g.ldr + n0 + cq + 8 * h);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) res[8 * h + i] = (float)x[i];
-        }
-    }
-  } else if constexpr (RMODE == 2) {
-    if (rok) {
-      float mu, rs;
-      dg_row_stats(g.r_stats + gr * 2 * ((N + 63) / 64), N, g.eps, mu, rs);
-      const float* zr = (const float*)g.r + gr * g.ldr;
-#pragma unroll
-      for (int c = 0; c < 16; c += 4) {
-        const long gc = n0 + cq + c;
-        if (gc < N) {
-          const f32x4 z = *(const f32x4*)(zr + gc), ga = *(const f32x4*)(g.r_gamma + gc),
-                      be = *(const f32x4*)(g.r_beta + gc);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) res[c + i] = (z[i] - mu) * rs * ga[i] + be[i];
-        }
-      }
-    }
-  }
-  const long p = g.cache ? *g.pos : 0;
   __syncthreads();
-  float v[16];
+  if (!epi) return;
+  float v[CPT];
 #pragma unroll
-  for (int c = 0; c < 16; c += 4) {
+  for (int c = 0; c < CPT; c += 4) {
     f32x4 a = *(const f32x4*)(red + r * DG_RLD + cq + c);
 #pragma unroll
-    for (int q = 1; q < 4; ++q) a += *(const f32x4*)(red + (q * 64 + r) * DG_RLD + cq + c);
+    for (int q = 1; q < NW; ++q) a += *(const f32x4*)(red + (q * BMR + r) * DG_RLD + cq + c);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float x = a[i] + bias[c + i];
@@ -465,23 +547,23 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(mit_decode_gemm_args g
       v[c + i] = x + res[c + i];
     }
   }
-  if (g.stats_out) {  // this tile's (mean, M2) per row over its valid columns; 4 lanes per row
+  if (g.stats_out) {  // this tile's (mean, M2) per row over its valid columns; TPR lanes per row
     const int nv = (int)min(64L, N - n0);
     float sm = 0.f;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) sm += (cq + c < nv) ? v[c] : 0.f;
-    sm += __shfl_xor(sm, 1, 64);
-    sm += __shfl_xor(sm, 2, 64);
+    for (int c = 0; c < CPT; ++c) sm += (cq + c < nv) ? v[c] : 0.f;
+#pragma unroll
+    for (int x = 1; x < TPR; x <<= 1) sm += __shfl_xor(sm, x, 64);
     const float mp = sm / (float)nv;
     float q2 = 0.f;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
+    for (int c = 0; c < CPT; ++c) {
       const float dv = v[c] - mp;
       q2 += (cq + c < nv) ? dv * dv : 0.f;
     }
-    q2 += __shfl_xor(q2, 1, 64);
-    q2 += __shfl_xor(q2, 2, 64);
-    if (rok && (tid & 3) == 0) {
+#pragma unroll
+    for (int x = 1; x < TPR; x <<= 1) q2 += __shfl_xor(q2, x, 64);
+    if (rok && (tid % TPR) == 0) {
       float* so = g.stats_out + (gr * nbn + bn) * 2;
       so[0] = mp;
       so[1] = q2;
@@ -489,10 +571,10 @@ __global__ __launch_bounds__(256) void decode_gemm_kernel(mit_decode_gemm_args g
   }
   if (!rok) return;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const long gc = n0 + cq + 8 * h;
+  for (int h = 0; h < CPT; h += 8) {
+    const long gc = n0 + cq + h;
     if (gc >= N) continue;
-    const float* vv = v + 8 * h;
+    const float* vv = v + h;
     if (g.C) {
       if constexpr (CF32) {
         float* o = (float*)g.C + gr * g.ldc + gc;
@@ -580,6 +662,23 @@ extern "C" int mit_attention_decode(int dtype, long B, long H, long Dh, const vo
                     (v_row * esz) % 16 == 0 && (v_batch * esz) % 16 == 0 && (o_batch * esz) % 16 == 0,
                 "mit_attention_decode: rows must be 16-B aligned");
   if (B <= 0 || H <= 0) return MIT_OK;
+  static int rows = -1;  // env MIT_DECODE_ROWS_ATTN=0: the (b, h)-block kernel everywhere (A/B)
+  if (rows < 0) rows = getenv("MIT_DECODE_ROWS_ATTN") ? atoi(getenv("MIT_DECODE_ROWS_ATTN")) : 1;
+  if (rows && dtype == MIT_BF16 && H * Dh == 512 && B < (1L << 31)) {
+#define MIT_ROWS_LAUNCH(DH_)                                                                                          \
+  hipLaunchKernelGGL((attn_decode_rows_kernel<DH_, 8>), dim3((unsigned)B), dim3(512), 0, (hipStream_t)stream,         \
+                     (const bf16*)q, q_batch, (const bf16*)k, k_row, k_batch, (const bf16*)v, v_row, v_batch, (bf16*)o, \
+                     o_batch, Lk, pos, key_tokens, tok_batch, pad_idx, scale)
+    switch (Dh) {
+      case 16: MIT_ROWS_LAUNCH(16); break;
+      case 32: MIT_ROWS_LAUNCH(32); break;
+      case 64: MIT_ROWS_LAUNCH(64); break;
+      default: MIT_ROWS_LAUNCH(128); break;
+    }
+#undef MIT_ROWS_LAUNCH
+    MIT_LAUNCH_CHECK("mit_attention_decode");
+    return MIT_OK;
+  }
 #define MIT_DECODE_LAUNCH(DH_)                                                                                       \
   DISPATCH_DT(dtype, hipLaunchKernelGGL((attn_decode_kernel<T, DH_>), dim3((unsigned)(B * H)), dim3(256), 0,          \
                                         (hipStream_t)stream, H, (const T*)q, q_batch, (const T*)k, k_row, k_batch,    \
@@ -645,19 +744,31 @@ extern "C" int mit_greedy_pick_advance(long B, long V, const float* logits, long
 }
 
 namespace {
-template <int AMODE, int ACT, int RMODE, bool CF32>
-int launch_decode_gemm(const mit_decode_gemm_args* g, hipStream_t s) {
-  const long nblk = ((g->M + 63) / 64) * ((g->N + 63) / 64);
-  const int lds = AMODE ? (int)max(64L * (g->K * 2 + 16) + 512, (long)DG_RED) : DG_RED;
+template <int AMODE, int ACT, int RMODE, bool CF32, int NW, int BMR>
+int launch_decode_gemm_nw(const mit_decode_gemm_args* g, hipStream_t s) {
+  const long nblk = ((g->M + BMR - 1) / BMR) * ((g->N + 63) / 64);
+  const int red = NW * BMR * DG_RLD * 4;
+  const int lds = AMODE ? (int)max(64L * (g->K * 2 + 16), (long)red) : red;
   static int attr = 0;
   if (attr < lds) {
-    (void)hipFuncSetAttribute((const void*)decode_gemm_kernel<AMODE, ACT, RMODE, CF32>,
+    (void)hipFuncSetAttribute((const void*)decode_gemm_kernel<AMODE, ACT, RMODE, CF32, NW, BMR>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = lds;
   }
-  hipLaunchKernelGGL((decode_gemm_kernel<AMODE, ACT, RMODE, CF32>), dim3((unsigned)nblk), dim3(256), lds, s, *g);
+  hipLaunchKernelGGL((decode_gemm_kernel<AMODE, ACT, RMODE, CF32, NW, BMR>), dim3((unsigned)nblk), dim3(NW * 64), lds, s, *g);
   MIT_LAUNCH_CHECK("mit_decode_gemm");
   return MIT_OK;
+}
+// long K on a bf16 operand (linear2, K = d_ff): 8 waves split it over 32 x 64 tiles (twice the
+// blocks, a quarter of the K steps per wave: the K loop is one L2 round trip per step)
+int g_dg_long = -1;  // env MIT_DECODE_LONGK=0: 4 waves, 64-row tiles for every K (A/B)
+template <int AMODE, int ACT, int RMODE, bool CF32>
+int launch_decode_gemm(const mit_decode_gemm_args* g, hipStream_t s) {
+  if (g_dg_long < 0) g_dg_long = getenv("MIT_DECODE_LONGK") ? atoi(getenv("MIT_DECODE_LONGK")) : 1;
+  if constexpr (AMODE == 0) {
+    if (g_dg_long && g->K >= 1024) return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 8, 32>(g, s);
+  }
+  return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 4, 64>(g, s);
 }
 }  // namespace
 

@@ -468,11 +468,12 @@ class ImageToTextModel:
         the image memory computed once, and ONE hipGraph-captured step replayed per token. The host
         checks the finished count every `check_every` tokens (the only synchronisation).
 
-        streams: the images are decoded as this many independent row groups, each with its own state
-        and graph, replayed on its own HIP stream so the groups' latency-bound launches overlap
-        (default: env MIT_DECODE_STREAMS, else 4 groups of >= 32 images). Rows never interact in
+        streams: the images are decoded as this many independent row groups, each with its own state,
+        issued on its own HIP stream (default: env MIT_DECODE_STREAMS, else 1). Rows never interact in
         greedy decoding and every kernel computes a row the same way at any batch size, so the ids
-        do not depend on the grouping."""
+        do not depend on the grouping. Measured at B = 256 (configs[4]): 2 / 3 / 4 groups take 1.12 /
+        1.23 / 1.53x the one-group time -- the groups' kernels do overlap, but every kernel boundary
+        costs the same whatever its size, so one group of full-width launches is fastest."""
         self.eval()
         pv = images if isinstance(images, torch.Tensor) else \
             self.image_processor(images=images, return_tensors="pt")["pixel_values"]
@@ -481,7 +482,7 @@ class ImageToTextModel:
         mem, mem_ld, S, _, _ = self._encode_memory(pv)
         dec = self.decoder
         if streams is None:
-            streams = int(os.environ.get("MIT_DECODE_STREAMS", "0")) or max(1, min(4, B // 32))
+            streams = int(os.environ.get("MIT_DECODE_STREAMS", "1"))
         G = max(1, min(int(streams), B))
         bounds = [B * i // G for i in range(G + 1)]
         states = [dec.decode_begin(mem[bounds[i] * S:bounds[i + 1] * S], mem_ld, S, bounds[i + 1] - bounds[i], max_len,
@@ -493,23 +494,40 @@ class ImageToTextModel:
             done = 1
             cur = torch.cuda.current_stream()
             side = [cur] + [torch.cuda.Stream(device=self.device) for _ in range(G - 1)]
-            if use_graph and steps > 1:
+            for s_ in side[1:]:
+                s_.wait_stream(cur)
+
+            def one_step():
+                for stt, s_ in zip(states, side):
+                    with torch.cuda.stream(s_):
+                        dec.decode_step(stt)
+            launch = os.environ.get("MIT_DECODE_LAUNCH", "plan") if use_graph else "eager"
+            if launch == "graph" and steps > 1:
+                # one hipGraph per group (ROCm launches a graph's nodes one by one from the host:
+                # ~8.7 us each, so the groups' graphs hardly overlap)
                 runs = []
                 for stt in states:
                     graph = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(graph):
                         dec.decode_step(stt)
                     runs.append(graph.replay)
+
+                def run():
+                    for r, s_ in zip(runs, side):
+                        with torch.cuda.stream(s_):
+                            r()
+            elif launch == "plan" and steps > 1:
+                # the step's launches recorded once (a real step) and re-issued from C++ (mit_plan_run,
+                # ~3.6 us per launch), every group on its own stream
+                prog = native.record(one_step)
+                done += 1
+                run = prog.run
             else:
-                runs = [(lambda s_=stt: dec.decode_step(s_)) for stt in states]
-            for s_ in side[1:]:
-                s_.wait_stream(cur)
+                run = one_step
             while done < steps:
                 n = min(check_every, steps - done)
                 for _ in range(n):
-                    for run, s_ in zip(runs, side):
-                        with torch.cuda.stream(s_):
-                            run()
+                    run()
                 done += n
                 if sum(int(stt.n_finished.item()) for stt in states) == B:
                     break

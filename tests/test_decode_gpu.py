@@ -62,20 +62,22 @@ def test_attention_decode_self_with_pad(dtype, lk, hd):
     assert (got - ref).abs().max().item() < tol
 
 
-def test_attention_decode_cross_fixed_lk():
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_attention_decode_cross_fixed_lk(dtype):
+    """fp32: the (b, h)-block kernel; bf16 at d = 512: the per-image row-streaming kernel."""
     B, H, S, d, L = 4, 8, 197, 512, 3
     g = torch.Generator().manual_seed(9)
     dev = torch.device("cuda")
-    q = torch.randn(B, d, generator=g).to(dev)
-    kv = torch.randn(B * S, L * 2 * d, generator=g).to(dev)
+    q = torch.randn(B, d, generator=g).to(dev, dtype)
+    kv = torch.randn(B * S, L * 2 * d, generator=g).to(dev, dtype)
     l = 1
     kvl = kv[:, l * 2 * d:]
-    o = torch.empty(B, d, device=dev)
+    o = torch.empty(B, d, device=dev, dtype=dtype)
     N.attention_decode(q, d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d, S * L * 2 * d, o, d, B, H, Lk=S)
     k = kv.view(B, S, L * 2 * d)[:, :, l * 2 * d:l * 2 * d + d].reshape(B, S, H, 64).cpu()
     v = kv.view(B, S, L * 2 * d)[:, :, l * 2 * d + d:l * 2 * d + 2 * d].reshape(B, S, H, 64).cpu()
     ref = _ref_attn(q.view(B, H, 64).cpu(), k, v, S).view(B, d)
-    assert (o.double().cpu() - ref).abs().max().item() < 1e-5
+    assert (o.double().cpu() - ref).abs().max().item() < (1e-5 if dtype == torch.float32 else 1e-2)
 
 
 def test_greedy_pick_first_max_and_end():
