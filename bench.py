@@ -112,7 +112,19 @@ class GemmProbe:
         self.rec.append((e0, e1, key, fl, nb))
         gc = type(g)()
         ctypes.memmove(ctypes.byref(gc), ctypes.byref(g), ctypes.sizeof(g))
-        self.step.append((key, gc, s, fl, nb))
+        self.step.append((key, lambda: native.gemm_relaunch(gc, s), s, fl, nb))
+
+    def grouped(self, flops, nbytes, launch):
+        """A grouped dW launch (native.gemm_grouped): launch() issues it on the current stream."""
+        import native
+        s = native.stream_ptr()
+        e0, e1 = HipEvent(), HipEvent()
+        e0.record(s)
+        launch()
+        e1.record(s)
+        key = ("gemm_bf16_grouped", 1, 1)
+        self.rec.append((e0, e1, key, flops, nbytes))
+        self.step.append((key, launch, s, flops, nbytes))
 
     def summary(self):
         """{(kernel, a_layout, b_layout): [seconds, flops, launches, algorithmic bytes]} from the in-place pairs."""
@@ -136,13 +148,15 @@ class GemmProbe:
         for key in sorted({k for k, *_ in self.step}):
             launches = [r for r in self.step if r[0] == key]
             s = launches[0][2]
-            for _, g, _, _, _ in launches:  # warm the code object / caches once
-                native.gemm_relaunch(g, s)
+            for _, relaunch, _, _, _ in launches:  # warm the code object / caches once
+                with native.on_stream(s):
+                    relaunch()
             e0, e1 = HipEvent(), HipEvent()
             e0.record(s)
             for _ in range(passes):
-                for _, g, _, _, _ in launches:
-                    native.gemm_relaunch(g, s)
+                for _, relaunch, _, _, _ in launches:
+                    with native.on_stream(s):
+                        relaunch()
             e1.record(s)
             torch.cuda.synchronize()
             n = passes * len(launches)
@@ -446,6 +460,8 @@ def main():
         role = {(0, 0): "NT: forward", (0, 1): "NN: dX", (1, 1): "TN: dW", (1, 0): "TT"}
 
         def names(k):
+            if k[0] == "gemm_bf16_grouped":
+                return "gemm_bf16_grouped (TN: a decoder layer's six dW, one launch + split-K combine)"
             return f"{k[0]}<{k[1]},{k[2]}> ({role[(k[1], k[2])]})"
         key = max(agg, key=lambda k: agg[k][0])
         t, fl, n, nb = agg[key]

@@ -120,6 +120,14 @@ int mit_gemm_set_fused_split(int on);
  * kernel, 0 for an empty problem) and stores the
  * split-K factor in *ksplit (may be NULL). For profiling tools that attribute kernel time. */
 int mit_gemm_plan(const mit_gemm_args* args, int* ksplit);
+/* Grouped weight-gradient GEMMs: n (<= 8) problems in ONE launch (+ one split-K combine launch),
+ * each a bf16 dW = dY^T X with both operands MN-contig, f32 output (alpha / accumulate honoured),
+ * optional fused bias-gradient rowsum, no other epilogue. Replaces a decoder layer's six
+ * nn.Linear / MHA weight gradients of autograd (torch/nn/functional.py linear backward), which at
+ * d_model 512 are 16-64-tile grids that each leave most CUs idle. The split-K factor is chosen for the
+ * group; workspace: >= mit_gemm_grouped_ws_bytes(args, n) bytes, 16-B aligned (no zero-fill needed). */
+long mit_gemm_grouped_ws_bytes(const mit_gemm_args* args, int n);
+int mit_gemm_grouped(const mit_gemm_args* args, int n, void* workspace, long workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * LayerNorm over the last dim, fp32 statistics.

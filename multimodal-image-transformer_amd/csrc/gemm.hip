@@ -31,6 +31,7 @@
 #include <stdlib.h>
 
 #include <cmath>
+#include <vector>
 
 #include "common.h"
 
@@ -330,12 +331,14 @@ __device__ __forceinline__ void wait_tiles(int younger) {
 // NST = LDS stages (K-tiles resident at once). Launched with 2 (64 KiB: two blocks per CU). Four
 // stages (three tiles in flight) on the 1-block-per-CU decoder grids measured no faster (within
 // 2 %, tools/gemm_bench.py): those blocks are bound by per-iteration latency, not DMA depth.
-template <int ALAY, int BLAY, int ACT, bool DROP, int NST, int NW = 4>
-__global__ __launch_bounds__(64 * NW) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
-                                                        long M, long N, long K, long lda, long ldb, long ldc,
-                                                        int a_bytes, int b_bytes, Epi e, int ksplit, long kchunk,
-                                                        float* __restrict__ ws, float* __restrict__ rowsum,
-                                                        int* __restrict__ tile_cnt, long ws_bytes) {
+// The body takes its block index (blk) so a grouped launch (gemm_bf16_grouped) can run several
+// problems' blocks in one grid.
+template <int ALAY, int BLAY, int ACT, bool DROP, int NST, int NW>
+__device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
+                                               long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
+                                               int b_bytes, const Epi& e, int ksplit, long kchunk,
+                                               float* __restrict__ ws, float* __restrict__ rowsum,
+                                               int* __restrict__ tile_cnt, long ws_bytes, int blk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // NW = 4: waves 2 (M) x 2 (N), 64x64 each; NW = 8: 4 (M) x 2 (N), 32x64 each (MI 16-row blocks)
   constexpr int NT = 64 * NW, WR = 128 / (NW / 2), MI = WR / 16;
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_bf16_kernel(const bf16* __restri
 
   const int nbn = (int)((N + BN - 1) / BN), nbm = (int)((M + BM - 1) / BM);
   const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
-  int bid = xcd_remap(blockIdx.x, nwg);
+  int bid = xcd_remap(blk, nwg);
   // split-K: slice `split` covers k in [kb, ke); a tile's slices are neighbours in the remapped
   // order, i.e. on one XCD (the in-launch combine below reads same-XCD slabs fastest)
   const int split = bid % ksplit;
@@ -523,6 +526,46 @@ __global__ __launch_bounds__(64 * NW) void gemm_bf16_kernel(const bf16* __restri
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     epi_row8<ACT, DROP>(e, C, ldc, N, gr, gc, v);
   }
+}
+
+template <int ALAY, int BLAY, int ACT, bool DROP, int NST, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
+                                                        long M, long N, long K, long lda, long ldb, long ldc,
+                                                        int a_bytes, int b_bytes, Epi e, int ksplit, long kchunk,
+                                                        float* __restrict__ ws, float* __restrict__ rowsum,
+                                                        int* __restrict__ tile_cnt, long ws_bytes) {
+  gemm_bf16_body<ALAY, BLAY, ACT, DROP, NST, NW>(A, B, C, M, N, K, lda, ldb, ldc, a_bytes, b_bytes, e, ksplit, kchunk,
+                                                ws, rowsum, tile_cnt, ws_bytes, blockIdx.x);
+}
+
+// Grouped weight-gradient GEMMs (dW = dY^T X, both operands MN-contig, f32 out, fused bias-gradient
+// row sums, optional split-K into fp32 slabs): one launch runs every problem's blocks (problem i owns
+// blocks [start_i, start_{i+1})), so a decoder layer's six small dW GEMMs (16-64 tiles each) fill the
+// chip together instead of one after another.
+constexpr int MAXG = 8;
+struct GroupProb {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  long M, N, K, lda, ldb, ldc;
+  int a_bytes, b_bytes, ksplit, start, rblocks, rstart;
+  long kchunk;
+  float* ws;
+  float* rowsum;
+  Epi e;
+};
+struct GroupArgs {
+  GroupProb p[MAXG];
+  int n;
+};
+
+__global__ __launch_bounds__(512) void gemm_bf16_grouped(GroupArgs ga) {
+  int i = 0;
+  while (i + 1 < ga.n && (int)blockIdx.x >= ga.p[i + 1].start) ++i;
+  const GroupProb& q = ga.p[i];
+  gemm_bf16_body<MIT_MN_CONTIG, MIT_MN_CONTIG, MIT_ACT_NONE, false, 2, 8>(
+      q.A, q.B, q.C, q.M, q.N, q.K, q.lda, q.ldb, q.ldc, q.a_bytes, q.b_bytes, q.e, q.ksplit, q.kchunk, q.ws, q.rowsum,
+      nullptr, 0, (int)blockIdx.x - q.start);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1106,6 +1149,32 @@ __global__ void gemm_splitk_reduce(long M, long N, int ksplit, const float* __re
   }
 }
 
+// the split-K combine of a grouped launch: problem i's slabs summed by blocks [rstart_i, +rblocks_i)
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_grouped(GroupArgs ga) {
+  int i = 0;
+  while (i + 1 < ga.n && (int)blockIdx.x >= ga.p[i + 1].rstart) ++i;
+  const GroupProb& q = ga.p[i];
+  const long M = q.M, N = q.N, n4 = N / 4, total = M * n4;
+  const long b0 = (long)blockIdx.x - q.rstart, stride = (long)q.rblocks * blockDim.x;
+  for (long t = b0 * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const long r = t / n4, c = (t % n4) * 4;
+    f32x4 s = *(const f32x4*)(q.ws + r * N + c);
+    for (int k = 1; k < q.ksplit; ++k) s += *(const f32x4*)(q.ws + ((long)k * M + r) * N + c);
+    s *= q.e.alpha;
+    f32x4* o = (f32x4*)((float*)q.C + r * q.ldc + c);
+    if (q.e.accumulate) s += *o;
+    *o = s;
+  }
+  if (q.rowsum) {
+    const float* rw = q.ws + (long)q.ksplit * M * N;
+    for (long r = b0 * blockDim.x + threadIdx.x; r < M; r += stride) {
+      float s = 0.f;
+      for (int k = 0; k < q.ksplit; ++k) s += rw[(long)k * M + r];
+      q.rowsum[r] = s;
+    }
+  }
+}
+
 // split-K plan for a plain-epilogue bf16 GEMM: only when the output has too few 128x128 tiles to
 // fill 256 CUs and K is long (the weight-gradient shapes). Returns 1 (no split) otherwise.
 int g_split_target = -1;  // blocks the split aims for (env MIT_SPLITK_TARGET; 128 beat 512 / 256 / 64 by 0.8-4 % in the step: fewer fp32 slabs)
@@ -1542,5 +1611,99 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
     else launch_f32<1, 1>(g, e, s);
   }
   MIT_LAUNCH_CHECK("mit_gemm");
+  return MIT_OK;
+}
+
+extern "C" long mit_gemm_grouped_ws_bytes(const mit_gemm_args* args, int n) {
+  if (!args || n <= 0 || n > MAXG) return 0;
+  long tiles = 0;
+  for (int i = 0; i < n; ++i) tiles += ((args[i].M + BM - 1) / BM) * ((args[i].N + BN - 1) / BN);
+  long s = tiles > 0 ? max(1L, min(16L, (2L * num_cus()) / tiles)) : 1;
+  long bytes = WS_HDR;
+  for (int i = 0; i < n; ++i) {
+    const long si = max(1L, min(s, args[i].K / 512));
+    bytes += si > 1 ? (4L * si * args[i].M * args[i].N + 4L * si * args[i].M + 255) / 256 * 256 : 0;
+  }
+  return bytes;
+}
+
+// Grouped dW launch (see gemm_bf16_grouped): split-K factor chosen for the group (about two blocks
+// per CU over all problems), slabs of problem i at consecutive 256-B aligned offsets of workspace.
+extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, void* workspace, long workspace_bytes, void* stream) {
+  MIT_CHECK_ARG(args && n >= 1 && n <= MAXG, "mit_gemm_grouped: 1..%d problems", MAXG);
+  MIT_RECORD([v = std::vector<mit_gemm_args>(args, args + n), workspace, workspace_bytes, stream]() {
+    return mit_gemm_grouped(v.data(), (int)v.size(), workspace, workspace_bytes, stream);
+  });
+  MIT_CHECK_ARG(workspace_bytes >= mit_gemm_grouped_ws_bytes(args, n) && (workspace || workspace_bytes == 0) &&
+                    al16(workspace),
+                "mit_gemm_grouped: workspace too small (%ld < %ld)", workspace_bytes, mit_gemm_grouped_ws_bytes(args, n));
+  long tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    const mit_gemm_args* g = args + i;
+    MIT_CHECK_ARG(g->dtype == MIT_BF16 && g->a_layout == MIT_MN_CONTIG && g->b_layout == MIT_MN_CONTIG,
+                  "mit_gemm_grouped: problem %d: bf16 MN-contig operands (weight gradients) only", i);
+    MIT_CHECK_ARG(!g->bias && g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f && g->out_f32,
+                  "mit_gemm_grouped: problem %d: plain epilogue with an f32 output only", i);
+    MIT_CHECK_ARG(g->A && g->B && g->C && g->M > 0 && g->N > 0 && g->K > 0, "mit_gemm_grouped: problem %d: empty", i);
+    MIT_CHECK_ARG(g->lda >= g->M && g->ldb >= g->N && g->ldc >= g->N && g->lda % 8 == 0 && g->ldb % 8 == 0 &&
+                      g->M % 8 == 0 && g->N % 8 == 0 && g->ldc % 4 == 0 && al16(g->A) && al16(g->B) && al16(g->C),
+                  "mit_gemm_grouped: problem %d: extents / alignment", i);
+    MIT_CHECK_ARG(2 * ((g->K - 1) * g->lda + g->M) < (1L << 31) && 2 * ((g->K - 1) * g->ldb + g->N) < (1L << 31),
+                  "mit_gemm_grouped: problem %d: operand spans >= 2 GiB", i);
+    tiles += ((g->M + BM - 1) / BM) * ((g->N + BN - 1) / BN);
+  }
+  const long s = max(1L, min(16L, (2L * num_cus()) / tiles));
+  GroupArgs ga;
+  ga.n = n;
+  int start = 0, rstart = 0;
+  bool any_split = false;
+  char* wsp = (char*)workspace + WS_HDR;
+  for (int i = 0; i < n; ++i) {
+    const mit_gemm_args* g = args + i;
+    GroupProb& q = ga.p[i];
+    q.A = (const bf16*)g->A;
+    q.B = (const bf16*)g->B;
+    q.C = g->C;
+    q.M = g->M; q.N = g->N; q.K = g->K; q.lda = g->lda; q.ldb = g->ldb; q.ldc = g->ldc;
+    q.a_bytes = (int)(2 * ((g->K - 1) * g->lda + g->M));
+    q.b_bytes = (int)(2 * ((g->K - 1) * g->ldb + g->N));
+    long si = max(1L, min(s, g->K / 512));
+    long kc = (g->K + si - 1) / si;
+    kc = (kc + BK - 1) / BK * BK;
+    si = (g->K + kc - 1) / kc;
+    q.ksplit = (int)si;
+    q.kchunk = kc;
+    q.rowsum = g->rowsum;
+    q.ws = nullptr;
+    if (si > 1) {
+      q.ws = (float*)wsp;
+      wsp += (4L * si * g->M * g->N + 4L * si * g->M + 255) / 256 * 256;
+      any_split = true;
+    }
+    Epi& e = q.e;
+    e = Epi{};
+    e.alpha = g->alpha;
+    e.act = MIT_ACT_NONE;
+    e.out_f32 = 1;
+    e.accumulate = g->accumulate;
+    e.vec = (g->N % 8 == 0) && (g->ldc % 8 == 0) && al16(g->C);
+    q.start = start;
+    start += (int)(((g->M + BM - 1) / BM) * ((g->N + BN - 1) / BN) * si);
+    q.rblocks = si > 1 ? (int)min(1024L, (g->M * (g->N / 4) + 255) / 256) : 0;
+    q.rstart = rstart;
+    rstart += q.rblocks;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  static bool attr = false;
+  if (!attr) {
+    set_lds(gemm_bf16_grouped, smem_bytes(2));
+    attr = true;
+  }
+  hipLaunchKernelGGL(gemm_bf16_grouped, dim3((unsigned)start), dim3(512), smem_bytes(2), st, ga);
+  MIT_LAUNCH_CHECK("mit_gemm_grouped");
+  if (any_split) {
+    hipLaunchKernelGGL(gemm_splitk_reduce_grouped, dim3((unsigned)rstart), dim3(256), 0, st, ga);
+    MIT_LAUNCH_CHECK("mit_gemm_grouped");
+  }
   return MIT_OK;
 }

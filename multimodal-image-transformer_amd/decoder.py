@@ -193,6 +193,13 @@ class _Acts:
             self.emb_plan = torch.empty(native.embed_plan_ints(R), dtype=torch.int32, device=dev)
             # the weight-gradient GEMMs run on a side stream (_SideStream) with their own scratch
             self.gemm_ws_side = torch.zeros(max(need, 4096) // 4 + 4, dtype=torch.float32, device=dev)
+            # grouped per-layer dW (TransformerDecoder.dw_grouped): the six dY operands of a layer in their own
+            # buffers, two sets (layer parity) so layer l's grouped launch overlaps layer l-1's dX chain
+            self.gdy = [[e(R, d) for _ in range(3)] for _ in range(2)]
+            self.gdh = [e(R, F) for _ in range(2)]
+            self.gdq = [e(R, d) for _ in range(2)]
+            self.gdqkv = [e(R, 3 * d) for _ in range(2)]
+            self.gws = None  # allocated on first use (native.gemm_grouped_ws_bytes)
 
 
 class _SideStream:
@@ -322,6 +329,9 @@ class TransformerDecoder:
         self._acts: Dict[tuple, _Acts] = {}
         # weight-gradient GEMMs on a second stream (MIT_DW_SIDE_STREAM=0 disables, for A/B)
         self.dw_side_stream = os.environ.get("MIT_DW_SIDE_STREAM", "1") != "0"
+        # a decoder layer's six weight gradients as ONE grouped launch (native.gemm_grouped) on the side
+        # stream, bf16 only (MIT_DW_GROUPED=0: one GEMM each, as they become ready)
+        self.dw_grouped = os.environ.get("MIT_DW_GROUPED", "1") != "0"
         self._side = None
         self.side_priority = 0  # set by ImageToTextModel.train_step (high priority beside the encoder)
         if self._own_store:
@@ -509,11 +519,17 @@ class TransformerDecoder:
         native.gemm(dlogits, w("fc_out.weight"), A.dx, R, d, Vp, b_layout=MN, ldb=d, workspace=ws)
         ready("fc_out.weight", "fc_out.bias")
         ascale = 1.0 / (1.0 - p) if p > 0 else 1.0
+        grouped = side is not None and self.dw_grouped and self.dtype == torch.bfloat16
         for l in reversed(range(L)):
             pre = f"layers.{l}."
             base = 64 * l
             xs, z, stt = A.xs[l], A.z[l], A.st[l]
             xin = A.x0 if l == 0 else A.xs[l - 1][2]
+            if grouped:
+                self._layer_backward_grouped(l, A, tokens, seed, p, xs, z, stt, xin, S, mem_keys, g, w, ln_bwd, guard,
+                                             side)
+                ready(pre + "linear2.weight", pre + "norm1.bias")
+                continue
             # LN3 -> dz3 (dx, in place) and d(ffn_out) (dy)
             guard(A.dy)
             ln_bwd(l, 3, A.dx, z[2], stt[2], A.dy, base + 5)
@@ -580,6 +596,63 @@ class TransformerDecoder:
         ready("cross_kv.weight", last)
         if side is not None:
             side.join()
+
+    def _layer_backward_grouped(self, l, A, tokens, seed, p, xs, z, stt, xin, S, mem_keys, g, w, ln_bwd, guard, side):
+        """One decoder layer of run_backward with its six weight gradients issued as ONE grouped launch
+        (native.gemm_grouped) on the side stream after the layer's dX chain; the dY operands live in the
+        layer-parity buffers A.gdy / gdh / gdq / gdqkv until that launch has read them."""
+        B, T = tokens.shape
+        d, H, L, F, R = self.d, self.H, self.L, self.F, A.R
+        MN = native.MN_CONTIG
+        pre = f"layers.{l}."
+        base = 64 * l
+        sp = l % 2
+        dyF, dyC, dyS = A.gdy[sp]
+        dh, dq, dqkv = A.gdh[sp], A.gdq[sp], A.gdqkv[sp]
+        ascale = 1.0 / (1.0 - p) if p > 0 else 1.0
+        ws = A.gemm_ws
+        # LN3 -> dz3 (dx, in place) and d(ffn_out)
+        guard(dyF)
+        ln_bwd(l, 3, A.dx, z[2], stt[2], dyF, base + 5)
+        guard(dh)
+        native.gemm(dyF, w(pre + "linear2.weight"), dh, R, F, d, b_layout=MN, ldb=F, aux=A.h[l], ld_aux=F,
+                    aux_scale=ascale)
+        native.gemm(dh, w(pre + "linear1.weight"), A.dx, R, d, F, b_layout=MN, ldb=d, residual=A.dx, ldr=d, workspace=ws)
+        guard(dyC)
+        ln_bwd(l, 2, A.dx, z[1], stt[1], dyC, base + 3)
+        native.gemm(dyC, w(pre + "cross_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)
+        kvl, dkvl = A.kv[:, l * 2 * d:], A.dkv[:, l * 2 * d:]
+        ca = native.attn_args(A.qc[l], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d, S * L * 2 * d,
+                              A.oc[l], d, T * d, lse=A.lse_c[l], scale=1.0 / math.sqrt(self.hd), drop_p=p, seed=seed,
+                              site=base + 2, key_tokens=mem_keys, tok_batch=S, pad_idx=0)
+        cg = native.attn_grads(A.do, d, T * d, dq, d, T * d, dkvl, L * 2 * d, S * L * 2 * d, dkvl[:, d:], L * 2 * d,
+                               S * L * 2 * d, A.delta)
+        guard(dq)
+        native.attention_bwd(native.dtype_code(dq), B, H, T, S, ca, cg, Dh=self.hd)
+        native.gemm(dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d, workspace=ws)
+        guard(dyS)
+        ln_bwd(l, 1, A.dx, z[0], stt[0], dyS, base + 1)
+        native.gemm(dyS, w(pre + "self_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)
+        qkv = A.qkv[l]
+        sa = native.attn_args(qkv, 3 * d, T * 3 * d, qkv[:, d:], 3 * d, T * 3 * d, qkv[:, 2 * d:], 3 * d, T * 3 * d,
+                              A.os[l], d, T * d, lse=A.lse_s[l], key_tokens=tokens, tok_batch=T, pad_idx=self.pad_idx,
+                              causal=True, scale=1.0 / math.sqrt(self.hd), drop_p=p, seed=seed, site=base + 0)
+        sg = native.attn_grads(A.do, d, T * d, dqkv, 3 * d, T * 3 * d, dqkv[:, d:], 3 * d, T * 3 * d, dqkv[:, 2 * d:],
+                               3 * d, T * 3 * d, A.delta)
+        guard(dqkv)
+        native.attention_bwd(native.dtype_code(dq), B, H, T, T, sa, sg, Dh=self.hd)
+        native.gemm(dqkv, w(pre + "self_in.weight"), A.dx, R, d, 3 * d, b_layout=MN, ldb=d, residual=A.dx, ldr=d,
+                    workspace=ws)
+        probs = [(dyF, A.h[l], g(pre + "linear2.weight"), d, F, R, d, F, g(pre + "linear2.bias")),
+                 (dh, xs[1], g(pre + "linear1.weight"), F, d, R, F, d, g(pre + "linear1.bias")),
+                 (dyC, A.oc[l], g(pre + "cross_out.weight"), d, d, R, d, d, g(pre + "cross_out.bias")),
+                 (dq, xs[0], g(pre + "cross_q.weight"), d, d, R, d, d, g(pre + "cross_q.bias")),
+                 (dyS, A.os[l], g(pre + "self_out.weight"), d, d, R, d, d, g(pre + "self_out.bias")),
+                 (dqkv, xin, g(pre + "self_in.weight"), 3 * d, d, R, 3 * d, d, g(pre + "self_in.bias"))]
+        if A.gws is None:
+            A.gws = torch.empty((native.gemm_grouped_ws_bytes(probs) + 255) // 4, dtype=torch.float32,
+                                device=self.device)
+        side.run(lambda: native.gemm_grouped(probs, A.gws), reads=(dyF, dh, dyC, dq, dyS, dqkv))
 
     # --- batched greedy decoding with a KV cache (config 5) ---------------------------------------
     def decode_begin(self, mem: torch.Tensor, mem_ld: int, S: int, B: int, max_len: int, start_id: int,

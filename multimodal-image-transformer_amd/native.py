@@ -74,6 +74,8 @@ SIGNATURES = {
     "mit_gemm_set_variant": (I, [I]),
     "mit_gemm_plan": (I, [ctypes.POINTER(GemmArgs), ctypes.POINTER(I)]),
     "mit_gemm_set_fused_split": (I, [I]),
+    "mit_gemm_grouped_ws_bytes": (L, [ctypes.POINTER(GemmArgs), I]),
+    "mit_gemm_grouped": (I, [ctypes.POINTER(GemmArgs), I, vp, L, vp]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
@@ -328,6 +330,39 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
     _check(lib().mit_gemm(ctypes.byref(g), stream_ptr()), "mit_gemm")
     if probe is not None:
         probe.after(g)
+
+
+def _dw_args(problems):
+    arr = (GemmArgs * len(problems))()
+    for i, (A, B, C, M, N, K, lda, ldb, rowsum) in enumerate(problems):
+        if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16 or C.dtype != torch.float32:
+            raise NativeError("gemm_grouped: bf16 operands and f32 outputs")
+        arr[i] = GemmArgs(BF16, MN_CONTIG, MN_CONTIG, M, N, K, ptr(A), lda, ptr(B), ldb, ptr(C), C.stride(0), 1.0, None,
+                          ACT_NONE, None, 0, None, 0, 1.0, 0.0, None, 0, 1, 0, ptr(rowsum), None, 0)
+    return arr
+
+
+def gemm_grouped_ws_bytes(problems) -> int:
+    return lib().mit_gemm_grouped_ws_bytes(_dw_args(problems), len(problems))
+
+
+def gemm_grouped(problems, workspace):
+    """Weight gradients C_i[M_i, N_i] (f32) = A_i^T B_i of up to 8 problems in one launch
+    (mit_gemm_grouped): problems = [(A [K, M] bf16 (row stride lda), B [K, N] bf16 (ldb), C, M, N, K,
+    lda, ldb, rowsum f32 [M] or None)], rowsum_i = the bias gradient (row sums of A_i^T)."""
+    arr = _dw_args(problems)
+    wsb = workspace.numel() * workspace.element_size()
+
+    def launch():
+        _check(lib().mit_gemm_grouped(arr, len(problems), ptr(workspace), wsb, stream_ptr()), "mit_gemm_grouped")
+    probe = _gemm_probe
+    if probe is None:
+        launch()
+        return
+    # algorithmic: operands once, f32 output once
+    flops = sum(2.0 * M * N * K for _, _, _, M, N, K, _, _, _ in problems)
+    nbytes = sum(2 * K * (M + N) + 4 * M * N for _, _, _, M, N, K, _, _, _ in problems)
+    probe.grouped(flops, nbytes, launch)
 
 
 _gemm_probe = None

@@ -386,3 +386,39 @@ def test_cross_entropy_row_kernel(V, want_grad):
         assert torch.count_nonzero(g[::5]).item() == 0  # ignored rows
     else:
         assert torch.equal(g, logits)
+
+
+@pytest.mark.parametrize("R", [4032, 520])
+def test_gemm_grouped_weight_gradients_match_single_launches(R):
+    """mit_gemm_grouped (a decoder layer's six dW = dY^T X + bias row sums in one launch, split-K chosen
+    for the group) against float64 torch, and against the one-GEMM-per-problem launches."""
+    dev = torch.device("cuda")
+    d, F = 512, 2048
+    g = torch.Generator().manual_seed(R)
+    shapes = [(d, F), (F, d), (d, d), (d, d), (d, d), (3 * d, d)]  # (M = out features, N = in features)
+    probs, refs = [], []
+    for M, Nn in shapes:
+        A = torch.randn(R, M, generator=g).to(dev, torch.bfloat16)
+        B = torch.randn(R, Nn, generator=g).to(dev, torch.bfloat16)
+        C = torch.full((M, Nn), float("nan"), device=dev)
+        rs = torch.full((M,), float("nan"), device=dev)
+        probs.append((A, B, C, M, Nn, R, M, Nn, rs))
+        refs.append((A.double().cpu().t() @ B.double().cpu(), A.double().cpu().sum(0)))
+    ws = torch.empty((N.gemm_grouped_ws_bytes(probs) + 255) // 4, device=dev)
+    N.gemm_grouped(probs, ws)
+    for (A, B, C, M, Nn, K, lda, ldb, rs), (rc, rr) in zip(probs, refs):
+        assert (C.double().cpu() - rc).abs().max().item() < 1e-3 * rc.abs().max().item()
+        assert (rs.double().cpu() - rr).abs().max().item() < 1e-3 * max(1.0, rr.abs().max().item())
+        C1 = torch.empty_like(C)
+        rs1 = torch.empty_like(rs)
+        N.gemm(A, B, C1, M, Nn, K, a_layout=N.MN_CONTIG, b_layout=N.MN_CONTIG, lda=lda, ldb=ldb, rowsum=rs1,
+               workspace=N.gemm_workspace(M, Nn, K, dev))
+        assert torch.allclose(C, C1, rtol=1e-5, atol=1e-3) and torch.allclose(rs, rs1, rtol=1e-5, atol=1e-4)
+
+
+def test_gemm_grouped_rejects_unsupported():
+    dev = torch.device("cuda")
+    A = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
+    C = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)  # bf16 output: not a weight gradient
+    with pytest.raises(N.NativeError):
+        N.gemm_grouped([(A, A, C, 64, 64, 64, 64, 64, None)], torch.empty(1024, device=dev))

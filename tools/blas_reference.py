@@ -15,7 +15,7 @@ import native  # noqa: E402
 # token step of the configs[4] batched decode, B = 256 rows; not part of the train-step sum)
 SHAPES = [
     ("enc qkv", 12608, 2304, 768, 0, 0, 12), ("enc o+res", 12608, 768, 768, 0, 0, 12),
-    ("enc fc1+gelu", 12608, 3072, 768, 0, 0, 12), ("enc fc2+res", 12608, 768, 3072, 0, 0, 12),
+    ("enc fc1+gelu", 12608, 3072, 768, 0, 0, 12), ("enc fc1 plain", 12608, 3072, 768, 0, 0, 0), ("enc fc2+res", 12608, 768, 3072, 0, 0, 12),
     ("dec kv_all", 12608, 6144, 512, 0, 0, 1), ("dec self_in", 4032, 1536, 512, 0, 0, 6),
     ("dec d-out", 4032, 512, 512, 0, 0, 18), ("dec ffn1", 4032, 2048, 512, 0, 0, 6),
     ("dec ffn2", 4032, 512, 2048, 0, 0, 6), ("dec fc_out", 4032, 10000, 512, 0, 0, 1),
