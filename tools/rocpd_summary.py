@@ -55,12 +55,25 @@ def main():
         rows = sorted(csv.DictReader(open(a.trace_csv)), key=lambda r: int(r["Start_Timestamp"]))
         last = max(i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"])
         d = collections.defaultdict(list)
+        spans = collections.defaultdict(list)
         for r in rows[last + 1:]:
             m = re.search(r"(gemm256_kernel|gemm_bf16_kernel)<(\d), (\d)", r["Kernel_Name"])
             if m:
-                d[f"{m.group(1)}<{m.group(2)},{m.group(3)}>"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                k = f"{m.group(1)}<{m.group(2)},{m.group(3)}>"
+                d[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                spans[k].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        # the replay issues every kernel instance's launches back to back (a warm pass, then the timed
+        # passes): consecutive dispatches overlap (the next one's waves start while the last tiles of
+        # the previous drain), so the per-dispatch average over-counts what the bench's event pair
+        # spans; first start -> last end of the timed passes / their launches is the comparable number
+        def span_per_launch(v):
+            if len(v) < 8 or len(v) % 4:
+                return None
+            t = v[len(v) // 4:]
+            return round((t[-1][1] - t[0][0]) / len(t) / 1e3, 2)
         chk = {"source": "rocprofv3 --kernel-trace of bench.py: the roofline replay launches (after the last AdamW)",
                "avg_us_trace": {k: round(sum(v) / len(v) / 1e3, 2) for k, v in sorted(d.items())},
+               "span_per_launch_us_trace": {k: span_per_launch(v) for k, v in sorted(spans.items())},
                "launches_trace": {k: len(v) for k, v in sorted(d.items())}}
         if a.bench_json:
             line = [x for x in open(a.bench_json) if x.startswith("{")][-1]
