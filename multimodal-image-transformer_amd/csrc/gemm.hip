@@ -1614,11 +1614,23 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   return MIT_OK;
 }
 
+// group split-K factor: about one block per CU over all problems -- at cfg1 (224 tiles per layer, 216
+// for the cross-K/V + projection pair) no split: 12482-12503 pairs/s vs 12278-12433 with 2 (two blocks
+// per CU), 12232-12263 with 3, 12081-12153 with 4 (interleaved, one box); the fp32 slabs and their
+// combine cost more than the shorter K loops save once the group fills the chip. Env
+// MIT_GROUPED_SPLIT overrides (A/B).
+long grouped_split(long tiles) {
+  static long forced = -1;
+  if (forced < 0) forced = getenv("MIT_GROUPED_SPLIT") ? atol(getenv("MIT_GROUPED_SPLIT")) : 0;
+  if (forced > 0) return min(forced, 16L);
+  return tiles > 0 ? max(1L, min(16L, (long)num_cus() / tiles)) : 1;
+}
+
 extern "C" long mit_gemm_grouped_ws_bytes(const mit_gemm_args* args, int n) {
   if (!args || n <= 0 || n > MAXG) return 0;
   long tiles = 0;
   for (int i = 0; i < n; ++i) tiles += ((args[i].M + BM - 1) / BM) * ((args[i].N + BN - 1) / BN);
-  long s = tiles > 0 ? max(1L, min(16L, (2L * num_cus()) / tiles)) : 1;
+  long s = grouped_split(tiles);
   long bytes = WS_HDR;
   for (int i = 0; i < n; ++i) {
     const long si = max(1L, min(s, args[i].K / 512));
@@ -1652,7 +1664,7 @@ extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, void* workspac
                   "mit_gemm_grouped: problem %d: operand spans >= 2 GiB", i);
     tiles += ((g->M + BM - 1) / BM) * ((g->N + BN - 1) / BN);
   }
-  const long s = max(1L, min(16L, (2L * num_cus()) / tiles));
+  const long s = grouped_split(tiles);
   GroupArgs ga;
   ga.n = n;
   int start = 0, rstart = 0;

@@ -200,6 +200,7 @@ class _Acts:
             self.gdq = [e(R, d) for _ in range(2)]
             self.gdqkv = [e(R, 3 * d) for _ in range(2)]
             self.gws = None  # allocated on first use (native.gemm_grouped_ws_bytes)
+            self.gws_tail = None  # the cross-K/V + projection pair
 
 
 class _SideStream:
@@ -579,7 +580,20 @@ class TransformerDecoder:
             ready(pre + "linear2.weight", pre + "norm1.bias")
         # cross K/V of all layers
         BS = B * S
-        dW(A.dkv, mem, "cross_kv.weight", "cross_kv.bias", L * 2 * d, d, BS, L * 2 * d, mem_ld)
+        pair = grouped and proj_input is not None
+        if pair:
+            # the memory gradient first, then the cross-K/V and projection weight gradients (the step's
+            # last GEMMs, on the critical path) as one grouped launch
+            enc_rows, enc_ld, E = proj_input
+            native.gemm(A.dkv, w("cross_kv.weight"), A.dmem, BS, d, L * 2 * d, b_layout=MN, ldb=d, workspace=ws)
+            tail = [(A.dkv, mem, g("cross_kv.weight"), L * 2 * d, d, BS, L * 2 * d, mem_ld, g("cross_kv.bias")),
+                    (A.dmem, enc_rows, g("projection.weight"), d, E, BS, d, enc_ld, g("projection.bias"))]
+            if A.gws_tail is None:
+                A.gws_tail = torch.empty((native.gemm_grouped_ws_bytes(tail) + 255) // 4, dtype=torch.float32,
+                                         device=self.device)
+            side.run(lambda: native.gemm_grouped(tail, A.gws_tail), reads=(A.dkv, A.dmem))
+        else:
+            dW(A.dkv, mem, "cross_kv.weight", "cross_kv.bias", L * 2 * d, d, BS, L * 2 * d, mem_ld)
         # embedding (scatter-add into a zeroed table gradient; PAD row gets nothing)
         ge = g("token_embedding.weight")
         native.zero(ge)
@@ -588,7 +602,9 @@ class TransformerDecoder:
         native.embed_bwd(tokens, A.dx, math.sqrt(d), ge, self.pad_idx, drop_p=p, seed=seed, site=EMB_SITE,
                          plan=A.emb_plan)
         last = "token_embedding.weight"
-        if proj_input is not None:
+        if pair:
+            last = "projection.bias"
+        elif proj_input is not None:
             enc_rows, enc_ld, E = proj_input
             native.gemm(A.dkv, w("cross_kv.weight"), A.dmem, BS, d, L * 2 * d, b_layout=MN, ldb=d, workspace=ws)
             dW(A.dmem, enc_rows, "projection.weight", "projection.bias", d, E, BS, d, enc_ld)
