@@ -126,8 +126,17 @@ int mit_gemm_plan(const mit_gemm_args* args, int* ksplit);
  * nn.Linear / MHA weight gradients of autograd (torch/nn/functional.py linear backward), which at
  * d_model 512 are 16-64-tile grids that each leave most CUs idle. The split-K factor is chosen for the
  * group; workspace: >= mit_gemm_grouped_ws_bytes(args, n) bytes, 16-B aligned (no zero-fill needed). */
+typedef struct {
+  long rows, cols;    /* the mit_layernorm_bwd call that left its partials in ws (dgamma == NULL) */
+  const float* ws;
+  float* dgamma;      /* f32 [cols], overwritten */
+  float* dbeta;
+} mit_ln_grads_job;
+/* ln (may be NULL, n_ln <= 4): LayerNorm parameter gradients reduced by extra blocks of the same grid
+ * (what mit_layernorm_param_grads does in its own launch) -- a decoder layer's three norms. */
 long mit_gemm_grouped_ws_bytes(const mit_gemm_args* args, int n);
-int mit_gemm_grouped(const mit_gemm_args* args, int n, void* workspace, long workspace_bytes, void* stream);
+int mit_gemm_grouped(const mit_gemm_args* args, int n, const mit_ln_grads_job* ln, int n_ln, void* workspace,
+                     long workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * LayerNorm over the last dim, fp32 statistics.

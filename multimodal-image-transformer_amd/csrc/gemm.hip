@@ -554,12 +554,52 @@ struct GroupProb {
   float* rowsum;
   Epi e;
 };
+// LayerNorm dgamma/dbeta column reductions riding in the same grid (the partials mit_layernorm_bwd
+// left in ws: nblk rows of [dgamma | dbeta]); 32 columns per block
+constexpr int MAXLN = 4;
+struct GroupLn {
+  const float* ws;
+  float* dgamma;
+  float* dbeta;
+  long nblk, cols;
+  int start;
+};
 struct GroupArgs {
   GroupProb p[MAXG];
-  int n;
+  GroupLn ln[MAXLN];
+  int n, nln, gemm_blocks;
 };
 
+__device__ __forceinline__ void ln_grads_block(const GroupLn& j, int blk) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float(*part)[33] = (float(*)[33])smem;
+  const int cl = threadIdx.x & 31, grp = threadIdx.x >> 5;  // 16 row groups x 32 columns
+  const long c = (long)blk * 32 + cl, w2 = 2 * j.cols;
+  float s = 0.f;
+  if (c < w2) {
+    long b = grp;
+    for (; b + 48 < j.nblk; b += 64)
+      s += (j.ws[b * w2 + c] + j.ws[(b + 16) * w2 + c]) + (j.ws[(b + 32) * w2 + c] + j.ws[(b + 48) * w2 + c]);
+    for (; b < j.nblk; b += 16) s += j.ws[b * w2 + c];
+  }
+  part[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && c < w2) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += part[g][cl];
+    if (c < j.cols) j.dgamma[c] = t;
+    else j.dbeta[c - j.cols] = t;
+  }
+}
+
 __global__ __launch_bounds__(512) void gemm_bf16_grouped(GroupArgs ga) {
+  if ((int)blockIdx.x >= ga.gemm_blocks) {
+    int j = 0;
+    while (j + 1 < ga.nln && (int)blockIdx.x >= ga.ln[j + 1].start) ++j;
+    ln_grads_block(ga.ln[j], (int)blockIdx.x - ga.ln[j].start);
+    return;
+  }
   int i = 0;
   while (i + 1 < ga.n && (int)blockIdx.x >= ga.p[i + 1].start) ++i;
   const GroupProb& q = ga.p[i];
@@ -1641,11 +1681,17 @@ extern "C" long mit_gemm_grouped_ws_bytes(const mit_gemm_args* args, int n) {
 
 // Grouped dW launch (see gemm_bf16_grouped): split-K factor chosen for the group (about two blocks
 // per CU over all problems), slabs of problem i at consecutive 256-B aligned offsets of workspace.
-extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, void* workspace, long workspace_bytes, void* stream) {
+extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, const mit_ln_grads_job* ln, int n_ln,
+                                void* workspace, long workspace_bytes, void* stream) {
   MIT_CHECK_ARG(args && n >= 1 && n <= MAXG, "mit_gemm_grouped: 1..%d problems", MAXG);
-  MIT_RECORD([v = std::vector<mit_gemm_args>(args, args + n), workspace, workspace_bytes, stream]() {
-    return mit_gemm_grouped(v.data(), (int)v.size(), workspace, workspace_bytes, stream);
+  MIT_CHECK_ARG(n_ln >= 0 && n_ln <= MAXLN && (n_ln == 0 || ln), "mit_gemm_grouped: 0..%d LayerNorm jobs", MAXLN);
+  MIT_RECORD([v = std::vector<mit_gemm_args>(args, args + n),
+              lv = std::vector<mit_ln_grads_job>(ln, ln + n_ln), workspace, workspace_bytes, stream]() {
+    return mit_gemm_grouped(v.data(), (int)v.size(), lv.data(), (int)lv.size(), workspace, workspace_bytes, stream);
   });
+  for (int j = 0; j < n_ln; ++j)
+    MIT_CHECK_ARG(ln[j].ws && ln[j].dgamma && ln[j].dbeta && ln[j].rows > 0 && ln[j].cols > 0,
+                  "mit_gemm_grouped: LayerNorm job %d: null pointer or empty", j);
   MIT_CHECK_ARG(workspace_bytes >= mit_gemm_grouped_ws_bytes(args, n) && (workspace || workspace_bytes == 0) &&
                     al16(workspace),
                 "mit_gemm_grouped: workspace too small (%ld < %ld)", workspace_bytes, mit_gemm_grouped_ws_bytes(args, n));
@@ -1710,6 +1756,18 @@ extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, void* workspac
   if (!attr) {
     set_lds(gemm_bf16_grouped, smem_bytes(2));
     attr = true;
+  }
+  ga.gemm_blocks = start;
+  ga.nln = n_ln;
+  for (int j = 0; j < n_ln; ++j) {
+    GroupLn& q = ga.ln[j];
+    q.ws = ln[j].ws;
+    q.dgamma = ln[j].dgamma;
+    q.dbeta = ln[j].dbeta;
+    q.cols = ln[j].cols;
+    q.nblk = mit_layernorm_bwd_ws_floats(ln[j].rows, ln[j].cols) / (2 * ln[j].cols);
+    q.start = start;
+    start += (int)((2 * ln[j].cols + 31) / 32);
   }
   hipLaunchKernelGGL(gemm_bf16_grouped, dim3((unsigned)start), dim3(512), smem_bytes(2), st, ga);
   MIT_LAUNCH_CHECK("mit_gemm_grouped");

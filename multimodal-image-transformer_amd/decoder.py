@@ -494,17 +494,21 @@ class TransformerDecoder:
             if side is not None:
                 side.guard(t)
 
-        def ln_bwd(l, k, dx, z, stt, dr, site):
-            """LayerNorm k (1..3) of layer l backward; dgamma/dbeta reduced on the side stream."""
+        def ln_bwd(l, k, dx, z, stt, dr, site, defer=False):
+            """LayerNorm k (1..3) of layer l backward; dgamma/dbeta reduced on the side stream (defer: the
+            reduction job is returned for the layer's grouped dW launch instead)."""
             gname, bname = f"layers.{l}.norm{k}.weight", f"layers.{l}.norm{k}.bias"
             if side is None:
                 native.layernorm_bwd(dx, z, stt[0], stt[1], st.p(gname), dx, g(gname), g(bname), A.ln_ws, dr=dr,
                                      drop_p=p, seed=seed, site=site)
-                return
+                return None
             ws_l = A.ln_ws_side[3 * l + k - 1]
             native.layernorm_bwd(dx, z, stt[0], stt[1], st.p(gname), dx, None, None, ws_l, dr=dr, drop_p=p, seed=seed,
                                  site=site)
+            if defer:
+                return (R, d, ws_l, g(gname), g(bname))
             side.run(lambda: native.layernorm_param_grads(R, d, ws_l, g(gname), g(bname)))
+            return None
 
         def ready(first, last):
             if grads_ready is None:
@@ -629,13 +633,13 @@ class TransformerDecoder:
         ws = A.gemm_ws
         # LN3 -> dz3 (dx, in place) and d(ffn_out)
         guard(dyF)
-        ln_bwd(l, 3, A.dx, z[2], stt[2], dyF, base + 5)
+        j3 = ln_bwd(l, 3, A.dx, z[2], stt[2], dyF, base + 5, defer=True)
         guard(dh)
         native.gemm(dyF, w(pre + "linear2.weight"), dh, R, F, d, b_layout=MN, ldb=F, aux=A.h[l], ld_aux=F,
                     aux_scale=ascale)
         native.gemm(dh, w(pre + "linear1.weight"), A.dx, R, d, F, b_layout=MN, ldb=d, residual=A.dx, ldr=d, workspace=ws)
         guard(dyC)
-        ln_bwd(l, 2, A.dx, z[1], stt[1], dyC, base + 3)
+        j2 = ln_bwd(l, 2, A.dx, z[1], stt[1], dyC, base + 3, defer=True)
         native.gemm(dyC, w(pre + "cross_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)
         kvl, dkvl = A.kv[:, l * 2 * d:], A.dkv[:, l * 2 * d:]
         ca = native.attn_args(A.qc[l], d, T * d, kvl, L * 2 * d, S * L * 2 * d, kvl[:, d:], L * 2 * d, S * L * 2 * d,
@@ -647,7 +651,7 @@ class TransformerDecoder:
         native.attention_bwd(native.dtype_code(dq), B, H, T, S, ca, cg, Dh=self.hd)
         native.gemm(dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d, workspace=ws)
         guard(dyS)
-        ln_bwd(l, 1, A.dx, z[0], stt[0], dyS, base + 1)
+        j1 = ln_bwd(l, 1, A.dx, z[0], stt[0], dyS, base + 1, defer=True)
         native.gemm(dyS, w(pre + "self_out.weight"), A.do, R, d, d, b_layout=MN, ldb=d, workspace=ws)
         qkv = A.qkv[l]
         sa = native.attn_args(qkv, 3 * d, T * 3 * d, qkv[:, d:], 3 * d, T * 3 * d, qkv[:, 2 * d:], 3 * d, T * 3 * d,
@@ -668,7 +672,7 @@ class TransformerDecoder:
         if A.gws is None:
             A.gws = torch.empty((native.gemm_grouped_ws_bytes(probs) + 255) // 4, dtype=torch.float32,
                                 device=self.device)
-        side.run(lambda: native.gemm_grouped(probs, A.gws), reads=(dyF, dh, dyC, dq, dyS, dqkv))
+        side.run(lambda: native.gemm_grouped(probs, A.gws, ln_jobs=(j3, j2, j1)), reads=(dyF, dh, dyC, dq, dyS, dqkv))
 
     # --- batched greedy decoding with a KV cache (config 5) ---------------------------------------
     def decode_begin(self, mem: torch.Tensor, mem_ld: int, S: int, B: int, max_len: int, start_id: int,

@@ -52,6 +52,10 @@ class DecodeGemmArgs(ctypes.Structure):
                 ("c_row", L), ("c_batch", L), ("kv_col0", L), ("pos", vp)]
 
 
+class LnGradsJob(ctypes.Structure):
+    _fields_ = [("rows", L), ("cols", L), ("ws", vp), ("dgamma", vp), ("dbeta", vp)]
+
+
 class AttnArgs(ctypes.Structure):
     _fields_ = [("q", vp), ("q_row", L), ("q_batch", L), ("k", vp), ("k_row", L), ("k_batch", L),
                 ("v", vp), ("v_row", L), ("v_batch", L), ("o", vp), ("o_row", L), ("o_batch", L),
@@ -75,7 +79,7 @@ SIGNATURES = {
     "mit_gemm_plan": (I, [ctypes.POINTER(GemmArgs), ctypes.POINTER(I)]),
     "mit_gemm_set_fused_split": (I, [I]),
     "mit_gemm_grouped_ws_bytes": (L, [ctypes.POINTER(GemmArgs), I]),
-    "mit_gemm_grouped": (I, [ctypes.POINTER(GemmArgs), I, vp, L, vp]),
+    "mit_gemm_grouped": (I, [ctypes.POINTER(GemmArgs), I, ctypes.POINTER(LnGradsJob), I, vp, L, vp]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
@@ -346,15 +350,21 @@ def gemm_grouped_ws_bytes(problems) -> int:
     return lib().mit_gemm_grouped_ws_bytes(_dw_args(problems), len(problems))
 
 
-def gemm_grouped(problems, workspace):
+def gemm_grouped(problems, workspace, ln_jobs=()):
     """Weight gradients C_i[M_i, N_i] (f32) = A_i^T B_i of up to 8 problems in one launch
     (mit_gemm_grouped): problems = [(A [K, M] bf16 (row stride lda), B [K, N] bf16 (ldb), C, M, N, K,
-    lda, ldb, rowsum f32 [M] or None)], rowsum_i = the bias gradient (row sums of A_i^T)."""
+    lda, ldb, rowsum f32 [M] or None)], rowsum_i = the bias gradient (row sums of A_i^T).
+    ln_jobs: up to 4 (rows, cols, ws, dgamma, dbeta) LayerNorm parameter reductions of partials that
+    layernorm_bwd(dgamma=None) left in ws, done by extra blocks of the same grid."""
     arr = _dw_args(problems)
+    jobs = (LnGradsJob * max(1, len(ln_jobs)))()
+    for i, (rows, cols, lws, dg, db) in enumerate(ln_jobs):
+        jobs[i] = LnGradsJob(rows, cols, ptr(lws), ptr(dg), ptr(db))
     wsb = workspace.numel() * workspace.element_size()
 
     def launch():
-        _check(lib().mit_gemm_grouped(arr, len(problems), ptr(workspace), wsb, stream_ptr()), "mit_gemm_grouped")
+        _check(lib().mit_gemm_grouped(arr, len(problems), jobs, len(ln_jobs), ptr(workspace), wsb, stream_ptr()),
+               "mit_gemm_grouped")
     probe = _gemm_probe
     if probe is None:
         launch()

@@ -422,3 +422,36 @@ def test_gemm_grouped_rejects_unsupported():
     C = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)  # bf16 output: not a weight gradient
     with pytest.raises(N.NativeError):
         N.gemm_grouped([(A, A, C, 64, 64, 64, 64, 64, None)], torch.empty(1024, device=dev))
+
+
+def test_gemm_grouped_folds_layernorm_param_grads():
+    """LayerNorm dgamma/dbeta jobs riding in the grouped launch equal mit_layernorm_param_grads bit for
+    bit (same per-column summation order)."""
+    dev = torch.device("cuda")
+    R, d = 4032, 512
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(R, d, generator=g).to(dev, torch.bfloat16)
+    B = torch.randn(R, d, generator=g).to(dev, torch.bfloat16)
+    C = torch.empty(d, d, device=dev)
+    jobs, want = [], []
+    for k in range(3):
+        z = torch.randn(R, d, generator=g).to(dev, torch.bfloat16)
+        dy = torch.randn(R, d, generator=g).to(dev, torch.bfloat16)
+        zf = z.float()
+        mean = zf.mean(-1)
+        rstd = torch.rsqrt(zf.var(-1, unbiased=False) + 1e-5)
+        gamma = torch.randn(d, generator=g).to(dev)
+        ws = torch.empty(N.layernorm_bwd_ws_floats(R, d), device=dev)
+        dx = torch.empty_like(dy)
+        N.layernorm_bwd(dy, z, mean, rstd, gamma, dx, None, None, ws)
+        dg, db = torch.full((d,), float("nan"), device=dev), torch.full((d,), float("nan"), device=dev)
+        rg, rb = torch.empty(d, device=dev), torch.empty(d, device=dev)
+        N.layernorm_param_grads(R, d, ws, rg, rb)
+        jobs.append((R, d, ws, dg, db))
+        want.append((rg, rb))
+    wsg = torch.empty((N.gemm_grouped_ws_bytes([(A, B, C, d, d, R, d, d, None)]) + 255) // 4, device=dev)
+    N.gemm_grouped([(A, B, C, d, d, R, d, d, None)], wsg, ln_jobs=jobs)
+    for (_, _, _, dg, db), (rg, rb) in zip(jobs, want):
+        assert torch.equal(dg, rg) and torch.equal(db, rb)
+    ref = A.double().cpu().t() @ B.double().cpu()
+    assert (C.double().cpu() - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
