@@ -1534,7 +1534,13 @@ Split plan_split(const mit_gemm_args* g) {
   // (9645 vs 9700 pairs/s) though 8-18 % faster alone. MIT_GEMM_FUSED_SPLIT=1 or
   // mit_gemm_set_fused_split(1) enables it.
   if (g_fused < 0) g_fused = getenv("MIT_GEMM_FUSED_SPLIT") && atoi(getenv("MIT_GEMM_FUSED_SPLIT")) != 0;
-  if (g_fused && !g->rowsum && !use_256(g->M, g->N, g->K, g->a_layout)) {
+  // long-K data gradients only (K-contig A, K >= MIT_GEMM_FUSED_MINK; 0 = off): the decoder's
+  // linear1 / self in_proj dX (K = d_ff / 3 d on 128 tiles) run 24-32 K-steps per block. Measured
+  // -1.0 % (1536) / -0.3 % (2048) in the step (interleaved, 3 rounds): off
+  static long fused_mink = -1;
+  if (fused_mink < 0) fused_mink = getenv("MIT_GEMM_FUSED_MINK") ? atol(getenv("MIT_GEMM_FUSED_MINK")) : 0;
+  const bool fused = g_fused || (fused_mink > 0 && g->K >= fused_mink && g->a_layout == MIT_K_CONTIG);
+  if (fused && !g->rowsum && !use_256(g->M, g->N, g->K, g->a_layout)) {
     const int s = fused_plan(g->M, g->N, g->K, &kc);
     if (s > 1 && fused_ws_bytes(g->M, g->N, s) <= g->workspace_bytes) {
       p.ks = s;
