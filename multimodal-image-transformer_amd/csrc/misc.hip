@@ -174,24 +174,40 @@ __global__ __launch_bounds__(256) void embed_bwd_seg_kernel(int n, int d, const 
   if (id == pad) return;
   const int lane = threadIdx.x & 63;
   const uint64_t key = dropout ? site_key(seed, site) : 0ull;
+  // a token's rows are summed in position order, ER rows' loads in flight at a time (the run of a
+  // token every caption has -- START at position 0 -- is B rows long: one dependent load per row
+  // made it the longest wave of the kernel)
+  constexpr int ER = 8;
   for (int c0 = lane * 8; c0 < d; c0 += 512) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int r = 0; r < len; ++r) {
-      const long j = perm[r];
-      float v[8];
-      if constexpr (sizeof(T) == 2) {
-        const bf16x8 x = *(const bf16x8*)(dx + j * d + c0);
+    for (int r0 = 0; r0 < len; r0 += ER) {
+      long jj[ER];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = (float)x[q];
-      } else {
-        const f32x4 x0 = *(const f32x4*)(dx + j * d + c0), x1 = *(const f32x4*)(dx + j * d + c0 + 4);
-        v[0] = x0[0]; v[1] = x0[1]; v[2] = x0[2]; v[3] = x0[3]; v[4] = x1[0]; v[5] = x1[1]; v[6] = x1[2]; v[7] = x1[3];
+      for (int u = 0; u < ER; ++u) jj[u] = r0 + u < len ? (long)perm[r0 + u] : -1;
+      float v[ER][8];
+#pragma unroll
+      for (int u = 0; u < ER; ++u) {
+        if (jj[u] < 0) continue;
+        const long j = jj[u];
+        if constexpr (sizeof(T) == 2) {
+          const bf16x8 x = *(const bf16x8*)(dx + j * d + c0);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[u][q] = (float)x[q];
+        } else {
+          const f32x4 x0 = *(const f32x4*)(dx + j * d + c0), x1 = *(const f32x4*)(dx + j * d + c0 + 4);
+          v[u][0] = x0[0]; v[u][1] = x0[1]; v[u][2] = x0[2]; v[u][3] = x0[3];
+          v[u][4] = x1[0]; v[u][5] = x1[1]; v[u][6] = x1[2]; v[u][7] = x1[3];
+        }
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float g = v[q] * scale;
-        if (dropout) g *= drop_mul(key, (uint64_t)(j * d + c0 + q), thresh, dscale);
-        acc[q] += g;
+      for (int u = 0; u < ER; ++u) {
+        if (jj[u] < 0) continue;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float g = v[u][q] * scale;
+          if (dropout) g *= drop_mul(key, (uint64_t)(jj[u] * d + c0 + q), thresh, dscale);
+          acc[q] += g;
+        }
       }
     }
     f32x4* o = (f32x4*)(dtable + id * d + c0);
