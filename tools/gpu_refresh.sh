@@ -1,4 +1,4 @@
-# Session-3 refresh on the current build: the bench lines of every BASELINE workload, then the
+# Refresh on the current build: the bench lines of every BASELINE workload, then the
 # rocprofv3 kernel trace + FETCH/WRITE passes (tools/profile_r02.sh)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/refresh

@@ -1,4 +1,4 @@
-# Round-2 GPU check: the -m gpu suite, then the bf16 parity table (tools/bf16_parity_report.py).
+# GPU check: the -m gpu suite, then the bf16 parity table (tools/bf16_parity_report.py).
 # A test failure (rc 1) still runs the report; any other status (fault, abort, timeout) stops.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
