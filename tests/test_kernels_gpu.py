@@ -119,7 +119,7 @@ def test_dropout_mask_and_gemm_dropout():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("cols", [128, 192, 512, 768, 1024])
+@pytest.mark.parametrize("cols", [128, 192, 200, 130, 512, 768, 1024])
 def test_layernorm_fwd_bwd(dtype, cols):
     rows = 200
     x = torch.randn(rows, cols, device=dev()).to(dtype)
