@@ -249,6 +249,105 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long rows, long cols, const
   }
 }
 
+// bf16 backward with 16-B loads / stores (8 columns per lane per 512-column pass, cols % 8 == 0,
+// cols <= 1024); same row mapping (BWD_ROWS rows per block, BWD_RPW per wave) and the same ws layout
+// of per-block column partials as ln_bwd_kernel (512 columns per LDS reduction pass)
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_wide_kernel(long rows, long cols, const bf16* dy, const bf16* __restrict__ z,
+                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                          const float* __restrict__ gamma, bf16* dx, bf16* dr,
+                                                          const uint64_t* seed, uint32_t site, uint32_t thresh,
+                                                          float dscale, int dropout, float* ws) {
+  __shared__ float red[4][2][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t key = dropout ? site_key(seed, site) : 0ull;
+  float pg[NV][8], pb[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pg[i][k] = pb[i][k] = 0.f;
+  const long r0 = (long)blockIdx.x * BWD_ROWS;
+  bf16x8 dd[BWD_RPW][NV], zv[BWD_RPW][NV];
+  float mus[BWD_RPW], rss[BWD_RPW];
+#pragma unroll
+  for (int j = 0; j < BWD_RPW; ++j) {
+    const long row = r0 + w + 4 * j;
+    const bool live = row < rows;
+    mus[j] = live ? mean[row] : 0.f;
+    rss[j] = live ? rstd[row] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const long c0 = (long)(i * 64 + lane) * 8;
+      const bool ok = live && c0 < cols;
+      dd[j][i] = ok ? *(const bf16x8*)(dy + row * cols + c0) : bf16x8{};
+      zv[j][i] = ok ? *(const bf16x8*)(z + row * cols + c0) : bf16x8{};
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < BWD_RPW; ++j) {
+    const long row = r0 + w + 4 * j;
+    if (row >= rows) break;
+    const float mu = mus[j], rs = rss[j];
+    float g[NV][8], xh[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const long c0 = (long)(i * 64 + lane) * 8;
+      const bool ok = c0 < cols;
+      const f32x4 g0 = ok ? *(const f32x4*)(gamma + c0) : f32x4{}, g1 = ok ? *(const f32x4*)(gamma + c0 + 4) : f32x4{};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = (float)dd[j][i][k];
+        const float ga = k < 4 ? g0[k] : g1[k - 4];
+        xh[i][k] = ok ? ((float)zv[j][i][k] - mu) * rs : 0.f;
+        g[i][k] = d * ga;
+        pg[i][k] += d * xh[i][k];
+        pb[i][k] += d;
+        s1 += g[i][k];
+        s2 += g[i][k] * xh[i][k];
+      }
+    }
+    s1 = wave_sum(s1) / (float)cols;
+    s2 = wave_sum(s2) / (float)cols;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const long c0 = (long)(i * 64 + lane) * 8;
+      if (c0 >= cols) continue;
+      bf16x8 o, om;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float v = rs * (g[i][k] - s1 - xh[i][k] * s2);
+        o[k] = (bf16)v;
+        om[k] = (bf16)(dropout ? v * drop_mul(key, (uint64_t)row * (uint64_t)cols + c0 + k, thresh, dscale) : v);
+      }
+      *(bf16x8*)(dx + row * cols + c0) = o;
+      if (dr) *(bf16x8*)(dr + row * cols + c0) = om;
+    }
+  }
+  // the 4 waves' column partials: one 512-column pass per i, 2 columns per thread
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[w][0][lane * 8 + k] = pg[i][k];
+      red[w][1][lane * 8 + k] = pb[i][k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int slot = threadIdx.x + 256 * h;
+      const long c = (long)i * 512 + slot;
+      if (c < cols) {
+        const float a = red[0][0][slot] + red[1][0][slot] + red[2][0][slot] + red[3][0][slot];
+        const float b = red[0][1][slot] + red[1][1][slot] + red[2][1][slot] + red[3][1][slot];
+        ws[(long)blockIdx.x * 2 * cols + c] = a;
+        ws[(long)blockIdx.x * 2 * cols + cols + c] = b;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // column-parallel sum of the block partials: 16 columns x 16 strided partial-row groups per block
 // (at 4032 rows x 512 columns: 252 partial rows, 64 blocks, 16 loads in flight per thread), then a
 // fixed-order LDS reduction over the groups (deterministic)
@@ -460,7 +559,17 @@ extern "C" int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy
                          (const T*)z, mean, rstd, gamma, (T*)dx, (T*)dr, seed, site, th, sc, dropout, ws);
     });
   };
-  if (dtype == MIT_BF16) {
+  static int wide = -1;  // env MIT_LN_WIDE=0: the 8-B-per-lane kernels for bf16 too (A/B)
+  if (wide < 0) wide = getenv("MIT_LN_WIDE") ? atoi(getenv("MIT_LN_WIDE")) : 1;
+  if (wide && dtype == MIT_BF16 && cols % 8 == 0 && cols <= 1024 &&
+      (((uintptr_t)dy | (uintptr_t)z | (uintptr_t)dx | (uintptr_t)dr | (uintptr_t)gamma) % 16) == 0) {
+    if (cols <= 512)
+      hipLaunchKernelGGL((ln_bwd_wide_kernel<1>), dim3((unsigned)nblk), dim3(256), 0, s, rows, cols, (const bf16*)dy,
+                         (const bf16*)z, mean, rstd, gamma, (bf16*)dx, (bf16*)dr, seed, site, th, sc, dropout, ws);
+    else
+      hipLaunchKernelGGL((ln_bwd_wide_kernel<2>), dim3((unsigned)nblk), dim3(256), 0, s, rows, cols, (const bf16*)dy,
+                         (const bf16*)z, mean, rstd, gamma, (bf16*)dx, (bf16*)dr, seed, site, th, sc, dropout, ws);
+  } else if (dtype == MIT_BF16) {
     if (vec) go(bf16(), std::true_type());
     else go(bf16(), std::false_type());
   } else {
