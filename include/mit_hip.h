@@ -109,7 +109,9 @@ int mit_gemm(const mit_gemm_args* args, void* stream);
 long mit_gemm_workspace_bytes(long M, long N, long K);
 /* Tile-kernel choice for bf16 GEMMs: 0 = per shape (default; env MIT_GEMM_VARIANT seeds it),
  * 1 = 128x128 kernel only, 2 = 256x256 kernel wherever split-K is not planned, 3 = the 64x64
- * register-streaming kernel for every NT GEMM without rowsum / split-K. Results are
+ * register-streaming kernel for every NT GEMM without rowsum / split-K, 5 / 6 = the 256-column
+ * kernel with 160 / 192-row tiles wherever it applies (K-contig A, gatherable epilogue: bit-identical
+ * to its 256-row tile; env MIT_G256_MI=5|6|8 forces the row count under 0). Results are
  * identical up to fp32 summation order; a tuning / test knob, not a numerics switch. */
 int mit_gemm_set_variant(int variant);
 /* In-launch split-K combine (see workspace above): 0 = off (default; env MIT_GEMM_FUSED_SPLIT=1

@@ -522,7 +522,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
     float m = -INFINITY, l = 0.f;
     const char* Kc = Ks;
     const char* Vc = Vs;
-    for (int j0 = 0; j0 < Lk; j0 += 64, Kc += 64 * 128, Vc += 64 * 128) {
+    int j0 = 0;
+    for (; j0 + 64 <= lkp; j0 += 64, Kc += 64 * 128, Vc += 64 * 128) {
       // ---- S^T = K Q^T for keys j0 .. j0+63 (4 key tiles of 16) ----
       f32x4 st[4];
 #pragma unroll
@@ -589,6 +590,77 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           ot[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv[hh][i]), pb, ot[i], 0, 0, 0);
+      }
+    }
+    // ---- tail: the last 16 / 32 / 48 keys (K/V are staged to a multiple of 16 rows, not 64) ----
+    const int ntail = (lkp - j0) >> 4;  // wave-uniform
+    if (ntail) {
+      f32x4 st[3];
+      float s[12];
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) {
+        if (nb < ntail) {
+          const u32x4 k0 = *(const u32x4*)(Kc + nb * 2048 + kofs);
+          const u32x4 k1 = *(const u32x4*)(Kc + nb * 2048 + kofs1);
+          st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k0), qf[0],
+                                                            f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k1), qf[1], st[nb], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          s[nb * 4 + t] = (nb < ntail && j0 + nb * 16 + g * 4 + t < Lk) ? st[nb][t] : -INFINITY;
+      }
+      float tmax = s[0];
+#pragma unroll
+      for (int k = 1; k < 12; ++k) tmax = __builtin_fmaxf(tmax, s[k]);
+      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = __builtin_fmaxf(m, tmax * sl2);  // finite: key j0 < Lk
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      float p[12], psum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        p[k] = __builtin_amdgcn_exp2f(fmaf(s[k], sl2, -mnew));
+        psum += p[k];
+      }
+      psum += __shfl_xor(psum, 16, 64);
+      psum += __shfl_xor(psum, 32, 64);
+      l = l * alpha + psum;
+      m = mnew;
+      if (DROP) {
+#pragma unroll
+        for (int nb = 0; nb < 3; ++nb)
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (nb < ntail)
+              p[nb * 4 + t] *= drop_mul(key, rowbase + (uint64_t)(j0 + nb * 16 + g * 4 + t), a.thresh, a.dscale);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ot[i] *= alpha;
+      if (ntail >= 2) {  // keys 0..31 of the tail: one 16x16x32 block per d-tile, as the main loop
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[j] = (bf16)p[j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + vofs[i][0]));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + vofs[i][1]));
+          const s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          ot[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pb, ot[i], 0, 0, 0);
+        }
+      }
+      if (ntail & 1) {  // the odd 16-key tile (tile 0 or 2): 16x16x16, k = g*4 + t on both operands
+        const int tb = ntail - 1;
+        const int voff = tb == 2 ? 4096 : 0;
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 pq;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) pq[t] = (bf16)p[(tb == 2 ? 8 : 0) + t];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + voff + vofs[i][0]));
+          ot[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(lo, __builtin_bit_cast(s16x4, pq), ot[i], 0, 0, 0);
+        }
       }
     }
     if (qlive) {
@@ -1071,11 +1143,16 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
     const long kb = 2 * ((Lk - 1) * x->k_row + D), vb = 2 * ((Lk - 1) * x->v_row + D);
     MIT_CHECK_ARG(kb < (1L << 31) && vb < (1L << 31), "mit_attention_fwd: K/V span >= 2 GiB");
     if (head_ok && !a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535) {
-      // head-resident K/V: one workgroup per (b, h), NW waves balanced over the 16-query tiles
-      const int lkp = (int)((Lk + 63) / 64 * 64);
+      // head-resident K/V: one workgroup per (b, h), NW waves balanced over the 16-query tiles.
+      // K/V rows are staged to a multiple of 16 (the key tail of < 64 runs 16-key tiles: a ViT-B/16
+      // head of 197 keys sweeps 208 instead of 256; 28.5 -> 27.7 us, tools/gpu_attn_ab.sh). <= 8 waves
+      // whenever two heads fit the LDS, so a CU holds two workgroups and one stages its K/V while the
+      // other computes. Three 5-wave workgroups per CU (one round of the 768 heads instead of 1.5,
+      // 52 KiB each) measured slower (30.8 us): the CU's VALU, not the rounds, bounds this kernel.
+      // The dropout instance is built for <= 512 threads. MIT_ATTN_PAD=64 restores the round-1 staging.
+      static const int pad = getenv("MIT_ATTN_PAD") ? atoi(getenv("MIT_ATTN_PAD")) : 16;
+      const int lkp = (int)((Lk + pad - 1) / pad * pad);
       const int nqt = (int)((Lq + 15) / 16);
-      // <= 8 waves whenever two heads fit the LDS, so a CU holds two workgroups and one stages its
-      // K/V while the other computes; the dropout instance is built for <= 512 threads
       const int maxw = (a.dropout || 2 * lkp * 256 <= 160 * 1024) ? 8 : 16;
       const int rounds = (nqt + maxw - 1) / maxw;
       const int nw = (nqt + rounds - 1) / rounds;

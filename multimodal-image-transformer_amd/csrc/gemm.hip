@@ -161,7 +161,7 @@ __device__ __forceinline__ void epi_row8(const Epi& e, void* C, long ldc, long N
 // residual (or aux mask) of all its segments, then only computes and stores. It covers every
 // epilogue except residual AND aux together, f32 accumulate and the non-vector (ragged ldc)
 // case, which keep the per-segment form (epi_row8).
-__device__ __forceinline__ bool epi_gatherable(const Epi& e) { return e.vec && !(e.res && e.aux) && !e.accumulate; }
+__host__ __device__ __forceinline__ bool epi_gatherable(const Epi& e) { return e.vec && !(e.res && e.aux) && !e.accumulate; }
 __device__ __forceinline__ void epi_bias8(const Epi& e, long c, long N, float* b) {
   if (e.bias && c < N) {
     const f32x4 b0 = *(const f32x4*)(e.bias + c), b1 = *(const f32x4*)(e.bias + c + 4);
@@ -643,7 +643,7 @@ constexpr int SMEM2_BYTES = (2 * BUF_BYTES > 8 * 64 * EPI_LD * 4) ? 2 * BUF_BYTE
 // byte offsets of this lane's two 16-B chunks in each half at K-tile 0 (OOB when the row / column
 // is out of range), the chunk's k inside the tile, and the per-K-tile byte step. Precomputed once
 // so the main loop issues each DMA with one compare and one add.
-template <int LAY>
+template <int LAY, int HR = 128>
 struct DmaPlan {
   uint32_t base[2][2];
   int kc[2];
@@ -656,9 +656,9 @@ struct DmaPlan {
         const int r = id >> 3, c = (id & 7) ^ ((r >> 1) & 7);
         kc[j] = c * 8;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const long row = row0 + h * 128 + r;
-          base[h][j] = row < rows_total ? (uint32_t)((row * ld + kb + c * 8) * 2) : OOB;
+        for (int h = 0; h < 2; ++h) {  // a half holds HR rows (rows HR..127 of its image load 0)
+          const long row = row0 + h * HR + r;
+          base[h][j] = (r < HR && row < rows_total) ? (uint32_t)((row * ld + kb + c * 8) * 2) : OOB;
         }
       } else {
         const int kr = id >> 4, c = (id & 15) ^ (mn_swz(kr) >> 4);
@@ -714,7 +714,11 @@ __device__ __forceinline__ void bar_raw() {
 #define MIT_G256_PRIO 1
 #endif
 
-template <int ALAY, int BLAY, int ACT, bool DROP>
+// MI = 16-row MFMA blocks per wave in M: 8 (256-row tiles) or 5 / 6 (160 / 192-row tiles, K-contig A
+// with the register epilogue only): the N = 768 / 1024 encoder GEMMs (o-proj, fc2) have 150 / 580
+// 256-row tiles -- one round on 150 of 256 CUs, or a third round for 68 tiles -- and shorter tiles fill
+// the rounds (mit_gemm picks per shape, tile_rounds_cost)
+template <int ALAY, int BLAY, int ACT, bool DROP, int MI = 8>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                       long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
                                                       int b_bytes, Epi e, int ksplit, long kchunk,
@@ -722,8 +726,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
+  static_assert(MI == 8 || (MI >= 4 && MI < 8 && ALAY == MIT_K_CONTIG), "gemm256_kernel: short tiles need K-contig A");
+  constexpr int HR = 16 * MI;          // rows per wave group = rows per A half-tile
+  constexpr int BMT = 2 * HR;          // tile rows
+  constexpr int IH0 = (MI + 1) / 2;    // row blocks in the wave's first row half (ih = 0)
 
-  const int nbn = (int)((N + B2 - 1) / B2), nbm = (int)((M + B2 - 1) / B2);
+  const int nbn = (int)((N + B2 - 1) / B2), nbm = (int)((M + BMT - 1) / BMT);
   const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
 #if MIT_G256_NOREMAP
   int bid = blockIdx.x;
@@ -739,14 +747,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   const int gsize = min(nbm - first_m, GROUP);
   const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
   const int bn = (bid % (GROUP * nbn)) / gsize;
-  const long m0 = (long)bm * B2, n0 = (long)bn * B2;
+  const long m0 = (long)bm * BMT, n0 = (long)bn * B2;
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
 
-  f32x4 acc[8][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -760,7 +768,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   const int nk = (int)((ke - kb + BK - 1) / BK);
-  DmaPlan<ALAY> pa;
+  DmaPlan<ALAY, HR> pa;
   DmaPlan<BLAY> pb;
   pa.init(lda, M, m0, kb, wid, lane);
   pb.init(ldb, N, n0, kb, wid, lane);
@@ -778,14 +786,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
-  bf16x8 af[4][2], blo[2][2], bhi[2][2];
-  auto read_a = [&](int buf, int ih) {  // A rows ih*64 .. +64 of this wave's 128
+  bf16x8 af[IH0][2], blo[2][2], bhi[2][2];
+  auto read_a = [&](int buf, int ih) {  // A row blocks [ih*IH0, ...) of this wave's MI (64 rows each half at MI = 8)
     const char* base = smem + buf * BUF_BYTES + wr * HALF_BYTES;
+    const int ni = ih ? MI - IH0 : IH0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < IH0; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag<ALAY>(base, ih * 64 + i * 16, kk, lane);
-    if (TN && do_rs) {
+      for (int kk = 0; kk < 2; ++kk)
+        if (i < ni) af[i][kk] = frag<ALAY>(base, (ih * IH0 + i) * 16, kk, lane);
+    if (TN && do_rs && MI == 8) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -800,16 +810,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       for (int kk = 0; kk < 2; ++kk) bf[j][kk] = frag<BLAY>(base, (wc & 1) * 64 + jh * 32 + j * 16, kk, lane);
   };
   auto mma = [&](int ih, int jh, bf16x8 (&bf)[2][2]) {
+    const int ni = ih ? MI - IH0 : IH0;
     if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < IH0; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[ih * 4 + i][jh * 2 + j] =
-              REG ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0)
-                  : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+          if (i < ni)
+            acc[ih * IH0 + i][jh * 2 + j] =
+                REG ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[ih * IH0 + i][jh * 2 + j], 0, 0, 0)
+                    : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * IH0 + i][jh * 2 + j], 0, 0, 0);
     if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
@@ -943,19 +955,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     // gathered register epilogue: v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane
     // group g with 8 consecutive columns: block 2jp + (g & 1), columns 8 * (g >> 1) .. +8
     const int g = lane >> 4;
-    const long r0 = m0 + wr * 128 + (lane & 15);
+    const long r0 = m0 + wr * HR + (lane & 15);
     const long c0 = n0 + wc * 64 + (g & 1) * 16 + (g >> 1) * 8;
     float b0[8], b1[8];
     epi_bias8(e, c0, N, b0);
     epi_bias8(e, c0 + 32, N, b1);
-    bf16x8 xs[8][2];
+    bf16x8 xs[MI][2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) xs[i][jp] = epi_x8(e, M, N, r0 + i * 16, c0 + jp * 32);
     const uint64_t key = epi_key<DROP>(e);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
         float v[8];
@@ -971,6 +983,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       }
     return;
   }
+  if constexpr (MI == 8) {  // short tiles launch only with the register epilogue (launch_bf16_256)
   if (wr == 0) bar_raw();  // re-align the groups
   bar_raw();
 
@@ -1042,6 +1055,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       epi_row8<ACT, DROP>(e, C, ldc, N, gr, gc, v);
     }
     __builtin_amdgcn_wave_barrier();
+  }
   }
 }
 
@@ -1397,22 +1411,67 @@ void launch_rs(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, h
                      (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
 }
 
-template <int AL, int BL, int ACT, bool DROP>
-void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
-  const long nbm = (g->M + B2 - 1) / B2, nbn = (g->N + B2 - 1) / B2;
+template <int AL, int BL, int ACT, bool DROP, int MI>
+void launch_256_mi(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  const long nbm = (g->M + 32 * MI - 1) / (32 * MI), nbn = (g->N + B2 - 1) / B2;
   static bool attr = false;
   if (!attr) {
-    set_lds(gemm256_kernel<AL, BL, ACT, DROP>, SMEM2_BYTES);
+    set_lds(gemm256_kernel<AL, BL, ACT, DROP, MI>, SMEM2_BYTES);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP>), dim3((unsigned)(nbm * nbn)), dim3(512), SMEM2_BYTES, s,
+  hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, MI>), dim3((unsigned)(nbm * nbn)), dim3(512), SMEM2_BYTES, s,
                      (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
                      b_bytes, e, 1, g->K, (float*)g->workspace, g->rowsum);
 }
 
 // 0 = pick per shape, 1 = always the 128x128 kernel, 2 = the 256x256 kernel wherever it has an
-// instance for the epilogue (tuning / tests)
+// instance for the epilogue, 3 = the register-streaming kernel where it applies, 5 / 6 = the
+// 256-column kernel with 160 / 192-row tiles where it applies (tuning / tests)
 int g_variant = -1;
+
+// rows per wave of the 256-column kernel: 16 x (8, 6 or 5). Short tiles need K-contig A and the
+// register epilogue; among those the fewest (rounds of one tile per CU) x (per-tile time) wins, the
+// per-tile time modelled as a fixed part + K-steps at a per-row-count rate (tools/gemm_bench.py)
+int gemm_variant();
+int tile_mi(const mit_gemm_args* g, const Epi& e) {
+  static const int forced = getenv("MIT_G256_MI") ? atoi(getenv("MIT_G256_MI")) : 0;
+  const bool shortok = g->a_layout == MIT_K_CONTIG && epi_gatherable(e);
+  if (!shortok) return 8;
+  const int v = gemm_variant();
+  if (v == 5 || v == 6) return v;
+  if (forced == 5 || forced == 6 || forced == 8) return forced;
+  const double cus = (double)num_cus(), nk = (double)((g->K + BK - 1) / BK), nbn = (double)((g->N + B2 - 1) / B2);
+  // per-tile K-step cost relative to MI = 8, measured on equal-round shapes (enc o / fc2, cfg3 o / fc2:
+  // 160-row tiles 0.98-0.99x the time of 256-row ones, 192-row 1.02-1.04x): the chip holds a lower
+  // clock when more CUs run MFMA loops, so shorter tiles pay only where they keep the round count
+  // (profiles/r02_gemm_short_tiles.txt)
+  const double FIX = 6.0, STEP = 1.54;  // us per tile, us per 64-deep K-step (MI = 8)
+  const int mis[3] = {8, 6, 5};
+  const double rate[3] = {1.0, 1.03, 0.975};
+  int best = 8;
+  double tbest = 1e30;
+  for (int i = 0; i < 3; ++i) {
+    const double tiles = (double)((g->M + 32 * mis[i] - 1) / (32 * mis[i])) * nbn;
+    const double t = std::ceil(tiles / cus) * (FIX + nk * STEP * rate[i]);
+    if (t < tbest * 0.995) {
+      tbest = t;
+      best = mis[i];
+    }
+  }
+  return best;
+}
+
+template <int AL, int BL, int ACT, bool DROP>
+void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  if constexpr (AL == MIT_K_CONTIG) {
+    switch (tile_mi(g, e)) {
+      case 6: return launch_256_mi<AL, BL, ACT, DROP, 6>(g, e, a_bytes, b_bytes, s);
+      case 5: return launch_256_mi<AL, BL, ACT, DROP, 5>(g, e, a_bytes, b_bytes, s);
+      default: break;
+    }
+  }
+  launch_256_mi<AL, BL, ACT, DROP, 8>(g, e, a_bytes, b_bytes, s);
+}
 int gemm_variant() {
   if (g_variant < 0) g_variant = getenv("MIT_GEMM_VARIANT") ? atoi(getenv("MIT_GEMM_VARIANT")) : 0;
   return g_variant;
@@ -1439,7 +1498,7 @@ bool use_rs(const mit_gemm_args* g) {
 bool use_256(long M, long N, long K, int a_layout) {
   const int v = gemm_variant();
   if (v == 1) return false;
-  if (v == 2) return true;
+  if (v == 2 || v == 5 || v == 6) return true;
   // the MN-contig-A instances (weight gradients) exceed 256 VGPRs and spill: 128 kernel (+ split-K)
   if (a_layout != MIT_K_CONTIG) return false;
   if (M < 256 || N < 256 || K < 128) return false;
@@ -1554,7 +1613,7 @@ Split plan_split(const mit_gemm_args* g) {
 }  // namespace
 
 extern "C" int mit_gemm_set_variant(int v) {
-  MIT_CHECK_ARG(v >= 0 && v <= 3, "mit_gemm_set_variant: %d not in {0,1,2,3}", v);
+  MIT_CHECK_ARG((v >= 0 && v <= 3) || v == 5 || v == 6, "mit_gemm_set_variant: %d not in {0,1,2,3,5,6}", v);
   g_variant = v;
   return MIT_OK;
 }

@@ -392,7 +392,8 @@ def set_gemm_probe(probe):
 
 def gemm_set_variant(v):
     """0 = per-shape tile-kernel choice, 1 = 128x128 only, 2 = 256x256 wherever legal, 3 = 64x64
-    register-streaming kernel for NT GEMMs."""
+    register-streaming kernel for NT GEMMs, 5 / 6 = the 256-column kernel with 160 / 192-row tiles
+    wherever legal (K-contig A, gatherable epilogue; else its 256-row tile)."""
     _check(lib().mit_gemm_set_variant(int(v)), "mit_gemm_set_variant")
 
 

@@ -203,3 +203,29 @@ def test_register_streaming_kernel(M, Nn, K):
     C2 = torch.empty_like(C)
     N.gemm(A, B, C2, M, Nn, K)
     assert torch.equal(C, C2), "register-streaming kernel not deterministic"
+
+
+@pytest.mark.parametrize("M,Nn,K", [(200, 264, 72), (961, 776, 200), (1000, 768, 3072), (12608, 768, 768)])
+@pytest.mark.parametrize("epi", ["plain", "bias_res", "gelu", "f32"])
+def test_gemm256_short_tiles_bit_identical(M, Nn, K, epi):
+    """160 / 192-row tiles (variants 5 / 6) run the same per-element MFMA K order as the 256-row tile,
+    so every epilogue's output is bit-identical, ragged M included."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(M, K, generator=g).to(dev(), torch.bfloat16)
+    w = (torch.randn(Nn, K, generator=g) / 10).to(dev(), torch.bfloat16)
+    kw = {}
+    if epi == "bias_res":
+        kw = dict(bias=torch.randn(Nn, generator=g).to(dev()), residual=torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16))
+    elif epi == "gelu":
+        kw = dict(bias=torch.randn(Nn, generator=g).to(dev()), act=N.ACT_GELU)
+    outs = {}
+    for v in (2, 6, 5):
+        N.gemm_set_variant(v)
+        C = torch.full((M, Nn), float("nan"), device=dev(), dtype=torch.float32 if epi == "f32" else torch.bfloat16)
+        N.gemm(x, w, C, M, Nn, K, **kw)
+        outs[v] = C
+    ref = x.float() @ w.float().t()
+    if epi == "plain" or epi == "f32":
+        assert _rel(outs[2], ref) < 8e-3
+    for v in (6, 5):
+        assert torch.equal(outs[v], outs[2]), f"variant {v}"

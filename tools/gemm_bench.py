@@ -22,6 +22,10 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("dX lin1+res", 4032, 512, 2048, 0, 1, "res0"), ("dX self_in+res", 4032, 512, 1536, 0, 1, "res0"),
     ("dX fc_out ws", 4032, 512, 10000, 0, 1, "ws"), ("dW dd ws", 512, 512, 4032, 1, 1, "ws"),
     ("dW ffn ws", 2048, 512, 4032, 1, 1, "ws"),
+    # CLIP ViT-L/14 encoder shapes: configs[2] (336 px, 577 tokens) and configs[3] (224 px, 257)
+    ("clip o+res", 36928, 1024, 1024, 0, 0, "res"), ("clip fc2+res", 36928, 1024, 4096, 0, 0, "res"),
+    ("clip qkv", 36928, 3072, 1024, 0, 0, "bias"), ("clip fc1+gelu", 36928, 4096, 1024, 0, 0, "gelu"),
+    ("cfg3 o+res", 16448, 1024, 1024, 0, 0, "res"), ("cfg3 fc2+res", 16448, 1024, 4096, 0, 0, "res"),
 ]
 
 
