@@ -111,7 +111,8 @@ long mit_gemm_workspace_bytes(long M, long N, long K);
  * 1 = 128x128 kernel only, 2 = 256x256 kernel wherever split-K is not planned, 3 = the 64x64
  * register-streaming kernel for every NT GEMM without rowsum / split-K, 5 / 6 = the 256-column
  * kernel with 160 / 192-row tiles wherever it applies (K-contig A, gatherable epilogue: bit-identical
- * to its 256-row tile; env MIT_G256_MI=5|6|8 forces the row count under 0). Results are
+ * to its 256-row tile; under 0 the 256-row tile, env MIT_G256_MI=5|6 forces a row count and -1 picks
+ * per shape). Results are
  * identical up to fp32 summation order; a tuning / test knob, not a numerics switch. */
 int mit_gemm_set_variant(int variant);
 /* In-launch split-K combine (see workspace above): 0 = off (default; env MIT_GEMM_FUSED_SPLIT=1

@@ -1439,7 +1439,12 @@ int tile_mi(const mit_gemm_args* g, const Epi& e) {
   if (!shortok) return 8;
   const int v = gemm_variant();
   if (v == 5 || v == 6) return v;
-  if (forced == 5 || forced == 6 || forced == 8) return forced;
+  if (forced == 5 || forced == 6) return forced;
+  // off by default: in the train step the encoder GEMMs run beside the decoder's kernels, and the
+  // 150-tile o-proj / fc2 grids leave 106 CUs to them -- 160-row tiles (237 blocks) measured 7 %
+  // slower end to end (11353-11414 vs 12205-12212 pairs/s interleaved) though 1-2 % faster alone.
+  // MIT_G256_MI=-1 enables the per-shape model below.
+  if (forced != -1) return 8;
   const double cus = (double)num_cus(), nk = (double)((g->K + BK - 1) / BK), nbn = (double)((g->N + B2 - 1) / B2);
   // per-tile K-step cost relative to MI = 8, measured on equal-round shapes (enc o / fc2, cfg3 o / fc2:
   // 160-row tiles 0.98-0.99x the time of 256-row ones, 192-row 1.02-1.04x): the chip holds a lower
