@@ -252,6 +252,12 @@ class VisionEncoder:
         """images f32 [B,3,H,W] (already normalised) -> last_hidden_state in the compute dtype.
         rows="all": [B, N, E] ; rows="cls": only the CLS rows are finalised, returned as the
         strided view [B, E] of the [B, N, E] buffer (row stride N*E)."""
+        return self.forward_split(images, rows, slot, self.L)()
+
+    def forward_split(self, images: torch.Tensor, rows: str = "all", slot: int = 0, split: int = 0):
+        """Launches the patch embedding and layers [0, split) now; returns rest() which launches
+        layers [split, L) and the final LayerNorm and returns forward()'s result. The prefetch stream
+        uses it to spread the frozen encoder over a step (model.prefetch_encoder)."""
         B = images.shape[0]
         if tuple(images.shape[1:]) != (3, self.image, self.image):
             raise ValueError(f"expected images [B,3,{self.image},{self.image}], got {tuple(images.shape)}")
@@ -268,7 +274,17 @@ class VisionEncoder:
             ws["h"] = h
         a, qkv, o, m = ws["a"], ws["qkv"], ws["o"], ws["m"]
         act = native.ACT_GELU if self.kind == "vit" else native.ACT_QUICK_GELU
-        for i in range(self.L):
+        split = max(0, min(self.L, split))
+        self._layers(B, ws, h, a, qkv, o, m, act, 0, split)
+
+        def rest():
+            self._layers(B, ws, h, a, qkv, o, m, act, split, self.L)
+            return self._finish(B, ws, h, rows)
+        return rest
+
+    def _layers(self, B, ws, h, a, qkv, o, m, act, i0, i1):
+        w, E, N, H = self.w, self.E, self.N, self.H
+        for i in range(i0, i1):
             native.layernorm_fwd(h, w[f"{i}.ln1.w"], w[f"{i}.ln1.b"], self.eps, a)
             native.linear(a, w[f"{i}.qkv.w"], qkv, bias=w[f"{i}.qkv.b"])
             args = native.attn_args(qkv, 3 * E, N * 3 * E, qkv[:, E:], 3 * E, N * 3 * E, qkv[:, 2 * E:], 3 * E,
@@ -278,6 +294,9 @@ class VisionEncoder:
             native.layernorm_fwd(h, w[f"{i}.ln2.w"], w[f"{i}.ln2.b"], self.eps, a)
             native.linear(a, w[f"{i}.fc1.w"], m, bias=w[f"{i}.fc1.b"], act=act)
             native.linear(m, w[f"{i}.fc2.w"], h, bias=w[f"{i}.fc2.b"], residual=h)
+
+    def _finish(self, B, ws, h, rows):
+        w, E, N = self.w, self.E, self.N
         if self.kind == "vit":
             out = ws["out"]
             if rows == "cls":

@@ -35,6 +35,13 @@ from params import FlatParams
 # previous encoder output for the same image tensor instead of recomputing it
 _PROFILE_REUSE_ENCODER = os.environ.get("MIT_PROFILE_REUSE_ENCODER") == "1"
 _STREAM_PRIORITY = os.environ.get("MIT_STREAM_PRIORITY", "0") == "1"  # measured neutral: opt-in
+# Prefetched encoder spread over the step: layers [0, MIT_ENC_SPLIT) start with the step, the rest
+# once the decoder forward is enqueued and done ("fwd") or after the backward ("bwd"); default: the
+# whole encoder at the start of the step (MIT_ENC_SPLIT unset). Measured neutral (split 6 / 9 after
+# the forward: +0.3 / +0.2 %, 11 after the backward: -1.1 %, tools/gpu_enc_split_ab.sh): the step is
+# bound by the CU-time of its kernels, not by where the encoder's launches sit in it
+_ENC_SPLIT = int(os.environ.get("MIT_ENC_SPLIT", "-1"))
+_ENC_GATE = os.environ.get("MIT_ENC_GATE", "fwd")
 
 
 def _high_priority() -> int:
@@ -147,6 +154,7 @@ class ImageToTextModel:
         self._enc_slot = 0
         self._prefetched = None
         self._last_pf = None
+        self._pf_rest = None
         self._hi_stream = None
         self._params: Optional["OrderedDict[str, torch.nn.Parameter]"] = None
         self._gen = 0  # bumped by every forward that writes the shared arenas (autograd staleness check)
@@ -212,6 +220,31 @@ class ImageToTextModel:
         enc = self.encoder.forward(images, rows="all", slot=slot)  # [B, N, E]
         return enc.reshape(B * N, E), E, N
 
+    def _encoder_rows_split(self, images: torch.Tensor, slot: int, split: int):
+        """_encoder_rows in two launch segments: layers [0, split) now, rest() -> (rows, ld, S)."""
+        B = images.shape[0]
+        N, E = self.encoder.N, self.encoder.E
+        cls = self.memory_mode == "cls"
+        rest = self.encoder.forward_split(images, rows="cls" if cls else "all", slot=slot, split=split)
+
+        def finish():
+            enc = rest()
+            return (enc, N * E, 1) if cls else (enc.reshape(B * N, E), E, N)
+        return finish
+
+    def _continue_prefetch(self):
+        """Launch the deferred encoder layers on the prefetch stream, after the main stream's work so far."""
+        if self._pf_rest is None:
+            return
+        rest, self._pf_rest = self._pf_rest, None
+        enc = self._enc_stream.cuda_stream
+        self._enc_events.wait_stream(enc, native.stream_ptr())
+        with torch.cuda.stream(self._enc_stream):
+            out = rest()
+        ev = self._enc_events.record(enc)
+        images, slot = self._prefetched[:2]
+        self._prefetched = self._last_pf = (images, slot, out, ev)
+
     def prefetch_encoder(self, images: torch.Tensor):
         """Start the frozen encoder's forward for the NEXT batch on a second stream; the next
         train_step(images) consumes it instead of recomputing. The encoder has no trainable state, so
@@ -228,6 +261,12 @@ class ImageToTextModel:
         enc = self._enc_stream.cuda_stream
         # the arena's previous reader (two steps back) is done: the encoder stream waits for main
         self._enc_events.wait_stream(enc, native.stream_ptr())
+        self._continue_prefetch()  # an earlier prefetch's deferred layers (not consumed by a step)
+        if 0 < _ENC_SPLIT < self.encoder.L:
+            with torch.cuda.stream(self._enc_stream):
+                self._pf_rest = self._encoder_rows_split(images, slot, _ENC_SPLIT)
+            self._prefetched = (images, slot, None, None)
+            return
         with torch.cuda.stream(self._enc_stream):
             out = self._encoder_rows(images, slot)
         ev = self._enc_events.record(enc)
@@ -240,6 +279,7 @@ class ImageToTextModel:
         E, d = self.encoder.E, self.decoder_embed_dim
         self.store.ensure_shadow()
         self._gen += 1
+        self._continue_prefetch()
         pf, self._prefetched = self._prefetched, None
         if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
             _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
@@ -368,6 +408,8 @@ class ImageToTextModel:
         A = dec.acts(B, T, S, True)
         native.step_inc(self.seed_t)
         logits, _ = dec.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, True)
+        if _ENC_GATE == "fwd":
+            self._continue_prefetch()
         native.zero(A.count)
         native.zero(A.loss_sum)
         native.count_targets(targets, self.decoder_pad_idx, A.count)
@@ -379,6 +421,8 @@ class ImageToTextModel:
         dec.run_backward(tokens, mem, mem_ld, S, A, self.seed_t, logits, proj_input=proj,
                          grads_ready=dist.grads_ready if dist is not None else None)
         native.scalar_div(A.loss_sum, A.count, A.loss)
+        if _ENC_GATE == "bwd":
+            self._continue_prefetch()
         if dist is not None:
             dist.finish_backward(A.loss)
         return A.loss
