@@ -338,7 +338,9 @@ def test_decode_gemm_rejects_bad_args():
 def test_greedy_pick_advance_moves_pos_once():
     dev = torch.device("cuda")
     B, V, T = 300, 777, 8
-    logits = torch.randn(B, V, device=dev)
+    g = torch.Generator().manual_seed(0)
+    logits = torch.randn(B, V, generator=g).to(dev)
+    logits[:, 5] = -1e9  # no row picks END (5): a finished row would write PAD in the later steps
     ids = torch.zeros(B, T, dtype=torch.int64, device=dev)
     ids2 = ids.clone()
     pos = torch.tensor([2], dtype=torch.int64, device=dev)
