@@ -390,7 +390,7 @@ void dispatch_nv(long cols, F&& f) {
 // bf16 rows with cols % 8 == 0, cols <= 1024 (every production width: 128 .. 1024): 16-B loads and
 // stores (8 columns per lane per 512-column pass) and RW rows per wave, all their loads issued before
 // the first reduction -- the 8-B-per-lane form moved 38.8 MB per encoder LayerNorm at ~3.5 TB/s
-template <int NV, int RW>
+template <int NV, int RW, bool HASR>
 __global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, const bf16* __restrict__ x, long ldx,
                                                           const bf16* __restrict__ r, long ldr, const uint64_t* seed,
                                                           uint32_t site, uint32_t thresh, float dscale, int dropout,
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, 
   const int lane = threadIdx.x & 63;
   const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RW;
   const uint64_t key = dropout ? site_key(seed, site) : 0ull;
-  bf16x8 xa[RW][NV], ra[RW][NV];
+  bf16x8 xa[RW][NV], ra[HASR ? RW : 1][NV];
 #pragma unroll
   for (int q = 0; q < RW; ++q)
 #pragma unroll
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, 
       const long c0 = (long)(i * 64 + lane) * 8, row = row0 + q;
       const bool ok = row < rows && c0 < cols;
       xa[q][i] = ok ? *(const bf16x8*)(x + row * ldx + c0) : bf16x8{};
-      if (r) ra[q][i] = ok ? *(const bf16x8*)(r + row * ldr + c0) : bf16x8{};
+      if (HASR) ra[q][i] = ok ? *(const bf16x8*)(r + row * ldr + c0) : bf16x8{};
     }
 #pragma unroll
   for (int q = 0; q < RW; ++q) {
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, 
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float a = (float)xa[q][i][k];
-        if (r) {
+        if (HASR) {
           float b = (float)ra[q][i][k];
           if (dropout) b *= drop_mul(key, (uint64_t)row * (uint64_t)cols + c0 + k, thresh, dscale);
           a += b;
@@ -495,16 +495,30 @@ extern "C" int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x,
   if (wide && dtype == MIT_BF16 && cols % 8 == 0 && cols <= 1024 && ldx % 8 == 0 && ldy % 8 == 0 &&
       (!r || ldr % 8 == 0) && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)r | (uintptr_t)z) % 16) == 0 &&
       ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0) {
-    constexpr int RW = 2;
-    const dim3 g2((unsigned)((rows + 4 * RW - 1) / (4 * RW)));
-    if (cols <= 512)
-      hipLaunchKernelGGL((ln_fwd_wide_kernel<1, RW>), g2, dim3(256), 0, s, rows, cols, (const bf16*)x, ldx,
-                         (const bf16*)r, ldr, seed, site, th, sc, dropout, gamma, beta, eps, (bf16*)z, (bf16*)y, ldy,
-                         mean, rstd);
-    else
-      hipLaunchKernelGGL((ln_fwd_wide_kernel<2, RW>), g2, dim3(256), 0, s, rows, cols, (const bf16*)x, ldx,
-                         (const bf16*)r, ldr, seed, site, th, sc, dropout, gamma, beta, eps, (bf16*)z, (bf16*)y, ldy,
-                         mean, rstd);
+    // RW rows per wave (env MIT_LN_RW = 1 / 2 / 4 for A/B). Alone (tools/ln_bench.py, interleaved):
+    // encoder 12608 x 768 9.4 / 10.2 / 11.6 us, CLIP-L 36928 x 1024 24.7 / 26.9 / 29.7 us, decoder
+    // 4032 x 512 + residual + dropout 6.3 / 6.5 / 8.7 us -- one row per wave: the most waves in flight
+    static const int rw_env = getenv("MIT_LN_RW") ? atoi(getenv("MIT_LN_RW")) : 0;
+    const int RWs = rw_env ? rw_env : 1;
+    auto launch = [&](auto nvc, auto rwc) {
+      constexpr int NVc = decltype(nvc)::value, RWc = decltype(rwc)::value;
+      const dim3 g2((unsigned)((rows + 4 * RWc - 1) / (4 * RWc)));
+      if (r)
+        hipLaunchKernelGGL((ln_fwd_wide_kernel<NVc, RWc, true>), g2, dim3(256), 0, s, rows, cols, (const bf16*)x, ldx,
+                           (const bf16*)r, ldr, seed, site, th, sc, dropout, gamma, beta, eps, (bf16*)z, (bf16*)y, ldy,
+                           mean, rstd);
+      else
+        hipLaunchKernelGGL((ln_fwd_wide_kernel<NVc, RWc, false>), g2, dim3(256), 0, s, rows, cols, (const bf16*)x, ldx,
+                           (const bf16*)r, ldr, seed, site, th, sc, dropout, gamma, beta, eps, (bf16*)z, (bf16*)y, ldy,
+                           mean, rstd);
+    };
+    auto by_rw = [&](auto nvc) {
+      if (RWs == 1) launch(nvc, std::integral_constant<int, 1>());
+      else if (RWs == 2) launch(nvc, std::integral_constant<int, 2>());
+      else launch(nvc, std::integral_constant<int, 4>());
+    };
+    if (cols <= 512) by_rw(std::integral_constant<int, 1>());
+    else by_rw(std::integral_constant<int, 2>());
     MIT_LAUNCH_CHECK("mit_layernorm_fwd");
     return MIT_OK;
   }

@@ -1,0 +1,42 @@
+"""Micro-benchmark of mit_layernorm_fwd on the train step's shapes (bf16): the encoder's pre-LN
+(12608 x 768, no residual) and the decoder's post-LN LN(x + dropout(r)) (4032 x 512). Prints us and
+TB/s of algorithmic bytes (x [+ r] read, y [+ z] written)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-image-transformer_amd"))
+import torch  # noqa: E402
+
+import native  # noqa: E402
+
+SHAPES = [("enc ln 768", 12608, 768, False), ("dec ln 512 +res+drop", 4032, 512, True), ("clip ln 1024", 36928, 1024, False)]
+
+
+def run(iters=50):
+    dev = torch.device("cuda")
+    for name, R, C, res in SHAPES:
+        x = torch.randn(R, C, device=dev).to(torch.bfloat16)
+        r = torch.randn(R, C, device=dev).to(torch.bfloat16) if res else None
+        y = torch.empty_like(x)
+        z = torch.empty_like(x) if res else None
+        g, b = torch.randn(C, device=dev), torch.randn(C, device=dev)
+        seed = torch.tensor([5], dtype=torch.int64, device=dev)
+        kw = dict(r=r, drop_p=0.1, seed=seed, site=3, z=z) if res else {}
+        for _ in range(5):
+            native.layernorm_fwd(x, g, b, 1e-5, y, **kw)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            native.layernorm_fwd(x, g, b, 1e-5, y, **kw)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / iters * 1e-3
+        nb = R * C * 2 * (4 if res else 2)
+        print(f"{name:22s} {R:6d} x {C:5d}  {t * 1e6:7.2f} us  {nb / t / 1e12:5.2f} TB/s", flush=True)
+
+
+if __name__ == "__main__":
+    native.load_library()
+    run()
