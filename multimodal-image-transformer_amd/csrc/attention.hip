@@ -461,6 +461,14 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
 // Dropout (decoder cross-attention in training) is a template flag.
 // ------------------------------------------------------------------------------------------------
 constexpr int HK_MAX = 640;  // keys per head the LDS can hold (K + V = 256 B per key)
+// lazy-rescale threshold of attn_fwd_head in log2 units (0 = rescale every chunk, the default). 8
+// measured ViT-B/16 27.3 -> 27.0 us, CLIP-L/14@336 47.3 -> 44.4 us, the cfg1 step neutral (12603 vs
+// 12612 pairs/s interleaved, tools/gpu_attn_lazy.sh), and it moved the cfg3 fixture's bf16 logits
+// error from 9.9e-3 to 1.03e-2, over the 1e-2 bound (rounding noise of P at another scale): off
+#ifndef MIT_ATTN_LAZY
+#define MIT_ATTN_LAZY 0
+#endif
+constexpr float LAZY_LOG2 = MIT_ATTN_LAZY;
 
 template <bool DROP>
 __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) void attn_fwd_head(long H, long Lq, long Lk, AttnK a, int kbytes, int vbytes,
@@ -560,18 +568,27 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
       for (int k = 1; k < 16; ++k) tmax = __builtin_fmaxf(tmax, s[k]);
       tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = __builtin_fmaxf(m, tmax * sl2);  // finite: >= 1 unmasked key per chunk
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      // lazy rescale (the kernel is VALU-bound): the running max m moves only when some row's chunk
+      // max exceeds it by more than LAZY_LOG2 (wave-uniform); otherwise p = 2^(s - m) <= 2^LAZY_LOG2,
+      // in range for bf16 P and the f32 sums, and l / O need no rescale. O = ot / l is unchanged.
+      const float cand = tmax * sl2;  // finite: >= 1 unmasked key per chunk
+      if (LAZY_LOG2 <= 0.f || __builtin_amdgcn_ballot_w64(cand > m + LAZY_LOG2) != 0ull) {
+        const float mnew = __builtin_fmaxf(m, cand);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ot[i] *= alpha;
+        m = mnew;
+      }
       float p[16], psum = 0.f;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        p[k] = __builtin_amdgcn_exp2f(fmaf(s[k], sl2, -mnew));
+        p[k] = __builtin_amdgcn_exp2f(fmaf(s[k], sl2, -m));
         psum += p[k];
       }
       psum += __shfl_xor(psum, 16, 64);
       psum += __shfl_xor(psum, 32, 64);
-      l = l * alpha + psum;
-      m = mnew;
+      l += psum;
       if (DROP) {
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb)
@@ -579,8 +596,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
           for (int t = 0; t < 4; ++t)
             p[nb * 4 + t] *= drop_mul(key, rowbase + (uint64_t)(j0 + nb * 16 + g * 4 + t), a.thresh, a.dscale);
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ot[i] *= alpha;
       // ---- O^T += V^T P^T, two 32-key halves ----
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
