@@ -201,6 +201,7 @@ class _Acts:
             self.gdqkv = [e(R, 3 * d) for _ in range(2)]
             self.gws = None  # allocated on first use (native.gemm_grouped_ws_bytes)
             self.gws_tail = None  # the cross-K/V + projection pair
+            self.gws_kv = None  # the cross-K/V weight gradient alone (TransformerDecoder.kv_dw_early)
 
 
 class _SideStream:
@@ -333,6 +334,10 @@ class TransformerDecoder:
         # a decoder layer's six weight gradients as ONE grouped launch (native.gemm_grouped) on the side
         # stream, bf16 only (MIT_DW_GROUPED=0: one GEMM each, as they become ready)
         self.dw_grouped = os.environ.get("MIT_DW_GROUPED", "1") != "0"
+        # the cross-K/V weight gradient (all layers' dY final once layer 0's cross-attention backward
+        # ran) goes out on the side stream right then, ahead of layer 0's grouped dW, instead of with
+        # the projection's after the memory gradient at the end of the backward
+        self.kv_dw_early = os.environ.get("MIT_KV_DW_EARLY", "1") != "0"
         self._side = None
         self.side_priority = 0  # set by ImageToTextModel.train_step (high priority beside the encoder)
         if self._own_store:
@@ -525,6 +530,18 @@ class TransformerDecoder:
         ready("fc_out.weight", "fc_out.bias")
         ascale = 1.0 / (1.0 - p) if p > 0 else 1.0
         grouped = side is not None and self.dw_grouped and self.dtype == torch.bfloat16
+        BS = B * S
+        pair = grouped and proj_input is not None
+        early = pair and self.kv_dw_early
+        kv_prob = (A.dkv, mem, g("cross_kv.weight"), L * 2 * d, d, BS, L * 2 * d, mem_ld, g("cross_kv.bias"))
+
+        def kv_early():
+            if not early:
+                return
+            if A.gws_kv is None:
+                A.gws_kv = torch.empty((native.gemm_grouped_ws_bytes([kv_prob]) + 255) // 4, dtype=torch.float32,
+                                       device=self.device)
+            side.run(lambda: native.gemm_grouped([kv_prob], A.gws_kv), reads=(A.dkv,))
         for l in reversed(range(L)):
             pre = f"layers.{l}."
             base = 64 * l
@@ -532,7 +549,7 @@ class TransformerDecoder:
             xin = A.x0 if l == 0 else A.xs[l - 1][2]
             if grouped:
                 self._layer_backward_grouped(l, A, tokens, seed, p, xs, z, stt, xin, S, mem_keys, g, w, ln_bwd, guard,
-                                             side)
+                                             side, after_cross=kv_early if l == 0 else None)
                 ready(pre + "linear2.weight", pre + "norm1.bias")
                 continue
             # LN3 -> dz3 (dx, in place) and d(ffn_out) (dy)
@@ -583,15 +600,13 @@ class TransformerDecoder:
                         ldr=d, workspace=ws)
             ready(pre + "linear2.weight", pre + "norm1.bias")
         # cross K/V of all layers
-        BS = B * S
-        pair = grouped and proj_input is not None
         if pair:
-            # the memory gradient first, then the cross-K/V and projection weight gradients (the step's
-            # last GEMMs, on the critical path) as one grouped launch
+            # the memory gradient first, then the projection weight gradient -- with the cross-K/V one
+            # as a group unless that went out early (kv_early) -- the step's last GEMMs
             enc_rows, enc_ld, E = proj_input
             native.gemm(A.dkv, w("cross_kv.weight"), A.dmem, BS, d, L * 2 * d, b_layout=MN, ldb=d, workspace=ws)
-            tail = [(A.dkv, mem, g("cross_kv.weight"), L * 2 * d, d, BS, L * 2 * d, mem_ld, g("cross_kv.bias")),
-                    (A.dmem, enc_rows, g("projection.weight"), d, E, BS, d, enc_ld, g("projection.bias"))]
+            tail = ([] if early else [kv_prob]) + [
+                (A.dmem, enc_rows, g("projection.weight"), d, E, BS, d, enc_ld, g("projection.bias"))]
             if A.gws_tail is None:
                 A.gws_tail = torch.empty((native.gemm_grouped_ws_bytes(tail) + 255) // 4, dtype=torch.float32,
                                          device=self.device)
@@ -617,7 +632,8 @@ class TransformerDecoder:
         if side is not None:
             side.join()
 
-    def _layer_backward_grouped(self, l, A, tokens, seed, p, xs, z, stt, xin, S, mem_keys, g, w, ln_bwd, guard, side):
+    def _layer_backward_grouped(self, l, A, tokens, seed, p, xs, z, stt, xin, S, mem_keys, g, w, ln_bwd, guard, side,
+                                after_cross=None):
         """One decoder layer of run_backward with its six weight gradients issued as ONE grouped launch
         (native.gemm_grouped) on the side stream after the layer's dX chain; the dY operands live in the
         layer-parity buffers A.gdy / gdh / gdq / gdqkv until that launch has read them."""
@@ -649,6 +665,8 @@ class TransformerDecoder:
                                S * L * 2 * d, A.delta)
         guard(dq)
         native.attention_bwd(native.dtype_code(dq), B, H, T, S, ca, cg, Dh=self.hd)
+        if after_cross is not None:
+            after_cross()
         native.gemm(dq, w(pre + "cross_q.weight"), A.dx, R, d, d, b_layout=MN, ldb=d, residual=A.dx, ldr=d, workspace=ws)
         guard(dyS)
         j1 = ln_bwd(l, 1, A.dx, z[0], stt[0], dyS, base + 1, defer=True)
