@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
 constexpr int HK_MAX = 640;  // keys per head the LDS can hold (K + V = 256 B per key)
 // lazy-rescale threshold of attn_fwd_head in log2 units (0 = rescale every chunk, the default). 8
 // measured ViT-B/16 27.3 -> 27.0 us, CLIP-L/14@336 47.3 -> 44.4 us, the cfg1 step neutral (12603 vs
-// 12612 pairs/s interleaved, tools/gpu_attn_lazy.sh), and it moved the cfg3 fixture's bf16 logits
+// 12612 pairs/s interleaved, tools/gpu_ab.sh -m attn_bench.py, MIT_HIP_LIB), and it moved the cfg3 fixture's bf16 logits
 // error from 9.9e-3 to 1.03e-2, over the 1e-2 bound (rounding noise of P at another scale): off
 #ifndef MIT_ATTN_LAZY
 #define MIT_ATTN_LAZY 0
@@ -1160,7 +1160,7 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
     if (head_ok && !a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535) {
       // head-resident K/V: one workgroup per (b, h), NW waves balanced over the 16-query tiles.
       // K/V rows are staged to a multiple of 16 (the key tail of < 64 runs 16-key tiles: a ViT-B/16
-      // head of 197 keys sweeps 208 instead of 256; 28.5 -> 27.7 us, tools/gpu_attn_ab.sh). <= 8 waves
+      // head of 197 keys sweeps 208 instead of 256; 28.5 -> 27.7 us, tools/gpu_ab.sh -m attn_bench.py MIT_ATTN_PAD=64 MIT_ATTN_PAD=16). <= 8 waves
       // whenever two heads fit the LDS, so a CU holds two workgroups and one stages its K/V while the
       // other computes. Three 5-wave workgroups per CU (one round of the 768 heads instead of 1.5,
       // 52 KiB each) measured slower (30.8 us): the CU's VALU, not the rounds, bounds this kernel.

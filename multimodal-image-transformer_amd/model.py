@@ -38,7 +38,7 @@ _STREAM_PRIORITY = os.environ.get("MIT_STREAM_PRIORITY", "0") == "1"  # measured
 # Prefetched encoder spread over the step: layers [0, MIT_ENC_SPLIT) start with the step, the rest
 # once the decoder forward is enqueued and done ("fwd") or after the backward ("bwd"); default: the
 # whole encoder at the start of the step (MIT_ENC_SPLIT unset). Measured neutral (split 6 / 9 after
-# the forward: +0.3 / +0.2 %, 11 after the backward: -1.1 %, tools/gpu_enc_split_ab.sh): the step is
+# the forward: +0.3 / +0.2 %, 11 after the backward: -1.1 %, tools/gpu_ab.sh -k prefetch): the step is
 # bound by the CU-time of its kernels, not by where the encoder's launches sit in it
 _ENC_SPLIT = int(os.environ.get("MIT_ENC_SPLIT", "-1"))
 _ENC_GATE = os.environ.get("MIT_ENC_GATE", "fwd")

@@ -1,22 +1,41 @@
 #!/bin/bash
 # Interleaved A/B of run-time knobs on ONE box (box-to-box spread is ~3 %, so only same-box,
 # interleaved rounds are compared):
-#   tools/gpu_ab.sh [-w WORKLOAD] [-r ROUNDS] "KNOB=a [KNOB2=b]" "KNOB=c" ...
-# Each variant is one bench.py run (--no-cpu-baseline --no-roofline) with those environment
-# assignments; prints "variant round value ms_per_step". The session-3 numbers in DESIGN §4.1c / §5.1
-# were taken this way, e.g. MIT_DW_GROUPED=1 / 0, MIT_GROUPED_SPLIT=1..4, MIT_STREAM_PRIORITY=0 / 1,
-# MIT_SPLITK_TARGET_DX=128 / 256 / 512, MIT_GEMM_FUSED_MINK=0 / 1536 / 2048, and for -w decode
+#   tools/gpu_ab.sh [-k PYTEST_EXPR] [-m MICRO_BENCH] [-w WORKLOAD] [-r ROUNDS] "KNOB=a [KNOB2=b]" "KNOB=c" ...
+# -k first runs the -m gpu tests matching PYTEST_EXPR ("all" = the whole suite) on the default build and
+# stops if they fail. Each variant is then one run with those environment assignments, R interleaved
+# rounds: of bench.py (--no-cpu-baseline --no-roofline; prints "variant round value ms_per_step"), or
+# with -m of a kernel micro-benchmark (tools/gemm_bench.py, attn_bench.py, ln_bench.py; a variant
+# "ARGS=..." passes its arguments, e.g. ARGS=2,6,5 for gemm_bench's tile variants). Variants may
+# select a library build with MIT_HIP_LIB=<path> (e.g. attention.hip built with -DMIT_ATTN_LAZY=8).
+# The numbers in DESIGN §4.1c / §4.1d / §5.1 were taken this way, e.g. MIT_DW_GROUPED, MIT_GROUPED_SPLIT,
+# MIT_STREAM_PRIORITY, MIT_SPLITK_TARGET(_DX), MIT_GEMM_FUSED_MINK, MIT_G256_MI, MIT_ATTN_PAD,
+# MIT_LN_RW / MIT_LN_WIDE, MIT_ENC_SPLIT / MIT_ENC_GATE, MIT_KV_DW_EARLY, and for -w decode
 # MIT_DECODE_FUSED, MIT_DECODE_LONGK, MIT_DECODE_ROWS_ATTN, MIT_DECODE_STREAMS, MIT_DECODE_LAUNCH.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-W=train; R=2
-while getopts "w:r:" o; do case $o in w) W=$OPTARG ;; r) R=$OPTARG ;; *) exit 2 ;; esac; done
+W=train; R=2; K=; MB=
+while getopts "k:m:w:r:" o; do
+  case $o in k) K=$OPTARG ;; m) MB=$OPTARG ;; w) W=$OPTARG ;; r) R=$OPTARG ;; *) exit 2 ;; esac
+done
 shift $((OPTIND - 1))
 OUT=gpurun_out/ab_$W
 mkdir -p $OUT
+if [ -n "$K" ]; then
+  SEL=(-k "$K"); [ "$K" = all ] && SEL=()
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -x "${SEL[@]}" --timeout 120 --timeout-method thread \
+    > $OUT/tests.log 2>&1
+  rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
+fi
 for r in $(seq 1 $R); do
   i=0
   for v in "$@"; do
     i=$((i + 1))
+    if [ -n "$MB" ]; then
+      echo "[$v] r$r"
+      args=$(echo "$v" | sed -n 's/.*ARGS=\([^ ]*\).*/\1/p')
+      env $(echo "$v" | sed 's/ARGS=[^ ]*//') timeout -k 10 300 python -u tools/$MB $args || exit 1
+      continue
+    fi
     env $v timeout -k 10 300 python -u bench.py --workload $W --no-cpu-baseline --no-roofline > $OUT/v$i.$r.json 2> $OUT/v$i.$r.err || exit 1
     echo "[$v] r$r $(python3 -c "import json;d=json.load(open('$OUT/v$i.$r.json'));print(d['value'], d['ms_per_step'])")"
   done
