@@ -42,6 +42,10 @@ _STREAM_PRIORITY = os.environ.get("MIT_STREAM_PRIORITY", "0") == "1"  # measured
 # bound by the CU-time of its kernels, not by where the encoder's launches sit in it
 _ENC_SPLIT = int(os.environ.get("MIT_ENC_SPLIT", "-1"))
 _ENC_GATE = os.environ.get("MIT_ENC_GATE", "fwd")
+# The prefetch that overwrites an arena slot waits only for the end of the backward of the step that
+# read it (a per-slot event), not for everything on the main stream: the encoder then runs beside
+# that step's clip + AdamW (HBM-bound) instead of after them. MIT_ENC_SLOT_EVENT=0: the old wait.
+_ENC_SLOT_EVENT = os.environ.get("MIT_ENC_SLOT_EVENT", "1") != "0"
 
 
 def _high_priority() -> int:
@@ -155,6 +159,8 @@ class ImageToTextModel:
         self._prefetched = None
         self._last_pf = None
         self._pf_rest = None
+        self._slot_free = None           # native.HipEvents(2): end of the backward of the step that read slot i
+        self._slot_freed = [False, False]  # slot i's event recorded since the slot was last read
         self._hi_stream = None
         self._params: Optional["OrderedDict[str, torch.nn.Parameter]"] = None
         self._gen = 0  # bumped by every forward that writes the shared arenas (autograd staleness check)
@@ -259,8 +265,12 @@ class ImageToTextModel:
         slot = 1 - self._enc_slot
         images = images.to(self.device, non_blocking=True)
         enc = self._enc_stream.cuda_stream
-        # the arena's previous reader (two steps back) is done: the encoder stream waits for main
-        self._enc_events.wait_stream(enc, native.stream_ptr())
+        # the arena's previous reader (two steps back) is done: the encoder stream waits for the end of
+        # that step's backward (its last read: the projection weight gradient), or for main
+        if _ENC_SLOT_EVENT and self._slot_freed[slot]:
+            native.HipEvents.wait(enc, self._slot_free.pool[slot])
+        else:
+            self._enc_events.wait_stream(enc, native.stream_ptr())
         self._continue_prefetch()  # an earlier prefetch's deferred layers (not consumed by a step)
         if 0 < _ENC_SPLIT < self.encoder.L:
             with torch.cuda.stream(self._enc_stream):
@@ -286,6 +296,7 @@ class ImageToTextModel:
             native.HipEvents.wait(native.stream_ptr(), ev)
         else:
             enc_rows, enc_ld, S = self._encoder_rows(images, self._enc_slot)
+        self._slot_freed[self._enc_slot] = False  # re-armed by _train_step once this step's readers are issued
         if not self.has_projection:
             return enc_rows, enc_ld, S, enc_rows, enc_ld
         key = (B, S)
@@ -420,6 +431,11 @@ class ImageToTextModel:
         proj = (enc_rows, enc_ld, self.encoder_output_dim) if self.has_projection else None
         dec.run_backward(tokens, mem, mem_ld, S, A, self.seed_t, logits, proj_input=proj,
                          grads_ready=dist.grads_ready if dist is not None else None)
+        if self._enc_stream is not None:  # this step's last reader of its encoder slot is issued
+            if self._slot_free is None:
+                self._slot_free = native.HipEvents(2)
+            self._slot_free.record_at(self._enc_slot, native.stream_ptr())
+            self._slot_freed[self._enc_slot] = True
         native.scalar_div(A.loss_sum, A.count, A.loss)
         if _ENC_GATE == "bwd":
             self._continue_prefetch()

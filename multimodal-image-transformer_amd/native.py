@@ -218,6 +218,11 @@ class HipEvents:
         _check(lib().mit_event_record(ev, stream), "mit_event_record")
         return ev
 
+    def record_at(self, i, stream):
+        """Record pool event i (a fixed edge, e.g. one per arena slot) on `stream`; returns it."""
+        _check(lib().mit_event_record(self.pool[i], stream), "mit_event_record")
+        return self.pool[i]
+
     @staticmethod
     def wait(stream, ev):
         _check(lib().mit_stream_wait_event(stream, ev), "mit_stream_wait_event")
