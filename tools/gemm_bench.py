@@ -35,7 +35,7 @@ def run(iters=20, variants=(1, 2)):
     res = []
     only = os.environ.get("GEMM_SHAPES")
     for name, M, N, K, al, bl, *epi in SHAPES:
-        if only and name not in only.split(","):
+        if only and name not in only.split(",") and name.replace(" ", "_") not in only.split(","):  # "_" for " "
             continue
         epi = epi[0] if epi else ""
         A = (torch.randn(M, K) if al == 0 else torch.randn(K, M)).to(dev, torch.bfloat16)
