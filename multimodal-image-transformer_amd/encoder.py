@@ -262,8 +262,7 @@ class VisionEncoder:
         if tuple(images.shape[1:]) != (3, self.image, self.image):
             raise ValueError(f"expected images [B,3,{self.image},{self.image}], got {tuple(images.shape)}")
         images = images.contiguous().float()
-        ws, w, E, N, H = self._workspace(B, slot), self.w, self.E, self.N, self.H
-        R = B * N
+        ws, w, E = self._workspace(B, slot), self.w, self.E
         native.im2col(images, ws["cols"], self.patch, self.kpad)
         native.linear(ws["cols"], w["patch.w"], ws["pt"], bias=w["patch.b"])
         h = ws["h"]
@@ -275,14 +274,14 @@ class VisionEncoder:
         a, qkv, o, m = ws["a"], ws["qkv"], ws["o"], ws["m"]
         act = native.ACT_GELU if self.kind == "vit" else native.ACT_QUICK_GELU
         split = max(0, min(self.L, split))
-        self._layers(B, ws, h, a, qkv, o, m, act, 0, split)
+        self._layers(B, h, a, qkv, o, m, act, 0, split)
 
         def rest():
-            self._layers(B, ws, h, a, qkv, o, m, act, split, self.L)
+            self._layers(B, h, a, qkv, o, m, act, split, self.L)
             return self._finish(B, ws, h, rows)
         return rest
 
-    def _layers(self, B, ws, h, a, qkv, o, m, act, i0, i1):
+    def _layers(self, B, h, a, qkv, o, m, act, i0, i1):
         w, E, N, H = self.w, self.E, self.N, self.H
         for i in range(i0, i1):
             native.layernorm_fwd(h, w[f"{i}.ln1.w"], w[f"{i}.ln1.b"], self.eps, a)
