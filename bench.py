@@ -46,7 +46,8 @@ class HipEvent:
     def __init__(self):
         import ctypes
         if HipEvent._hip is None:
-            h = ctypes.CDLL("libamdhip64.so.7")  # soname: resolves to the runtime torch already loaded
+            import native
+            h = native.hip_runtime()  # the runtime this process already maps
             h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
             h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
             h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
@@ -286,37 +287,146 @@ def cpu_baseline(model, args):
                      "configs[0] (2L d128 H8 + ViT-B/16, batch 4, seq_len 32, cls)": round(v_cfg0, 3)}}
 
 
-def bench_decode(args):
+def decode_throughput(args, launch=None):
     """configs[4]: greedy captions for a batch of images (ImageToTextModel.generate_batch). END is set
     to an id the vocabulary never produces, so every caption runs the full max_len - 1 tokens (fixed
-    work per call). One call = encoder forward + cross K/V + (max_len - 1) replayed token steps."""
-    torch.cuda.set_device(0)
-    dev = torch.device("cuda", 0)
-    args.memory_mode = "patches"
-    model, _ = build(args, 0)
+    work per call). One call = encoder forward + cross K/V + (max_len - 1) token steps, replayed as a
+    native launch plan (mit_plan_run) by default or as one hipGraph per step (launch="graph")."""
+    import model as model_mod  # noqa: F401  (generate_batch reads MIT_DECODE_LAUNCH per call)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    a = argparse.Namespace(**vars(args))
+    a.memory_mode, a.workload = "patches", "train"
+    model, _ = build(a, 0)
     model.eval()
     B = args.decode_batch
     images = synthetic_batch(B, 2, args.vocab, dev, 5)[0]
     never = args.vocab + 7
-    for _ in range(max(1, args.warmup // 2)):
-        model.generate_batch(images, 2, never, max_len=args.max_len)
+    old = os.environ.get("MIT_DECODE_LAUNCH")
+    if launch:
+        os.environ["MIT_DECODE_LAUNCH"] = launch
+    try:
+        for _ in range(max(1, args.warmup // 2)):
+            model.generate_batch(images, 2, never, max_len=args.max_len)
+        torch.cuda.synchronize()
+        K = max(1, args.steps // 4)
+        t0 = time.perf_counter()
+        for _ in range(K):
+            ids = model.generate_batch(images, 2, never, max_len=args.max_len)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    finally:
+        if launch:
+            if old is None:
+                os.environ.pop("MIT_DECODE_LAUNCH", None)
+            else:
+                os.environ["MIT_DECODE_LAUNCH"] = old
+    toks = B * (args.max_len - 1) * K
+    return {"value": round(toks / el, 1), "unit": "tokens/s", "calls": K, "ms_per_call": round(1e3 * el / K, 3),
+            "images_per_s": round(B * K / el, 2), "us_per_token_step": round(1e6 * el / K / (args.max_len - 1), 2),
+            "ids_per_caption": len(ids[0]), "images": B, "max_len": args.max_len,
+            "launch": launch or os.environ.get("MIT_DECODE_LAUNCH", "plan")}
+
+
+DECODE_LAUNCH_NOTE = ("per-token step replayed as a native launch plan (mit_plan_run: the step's launches recorded "
+                      "once, re-issued from C++); a hipGraph of the same step is the slower alternative on ROCm 7 "
+                      "(graph replay issues its nodes one by one, ~8.7 us each on the host) -- both are timed in "
+                      "the bench's `also` block")
+
+
+def bench_decode(args):
+    torch.cuda.set_device(0)
+    d = decode_throughput(args)
+    out = {"metric": "greedy caption tokens/sec (batched KV-cache decode, 6L/d512 decoder + ViT-B/16)",
+           "value": d["value"], "unit": "tokens/s", "n_gpus": 1, "steps": d["calls"], "warmup": max(1, args.warmup // 2),
+           "ms_per_step": d["ms_per_call"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": args.dtype, "data": "synthetic (randn 224x224 images; random-init weights)",
+           "config": {"workload": "configs[4]: inference.py greedy decode, cached cross-attn K/V, " + DECODE_LAUNCH_NOTE,
+                      "images": d["images"], "max_len": args.max_len, "memory_mode": "patches"},
+           "images_per_s": d["images_per_s"], "us_per_token_step": d["us_per_token_step"],
+           "ids_per_caption": d["ids_per_caption"]}
+    print(json.dumps(out), flush=True)
+
+
+def also_block(args):
+    """The other single-GPU BASELINE configs in the same run (N = 1, rank 0), after the headline line's
+    measurements: configs[2] (6L d512 decoder + CLIP ViT-L/14@336, 577 patches) train-step pairs/s over
+    a few replayed steps, and configs[4] (batched greedy decode, B = 256, max_len 100) tokens/s with the
+    default native launch plan and with one hipGraph per token step."""
+    import native
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = {}
+    t_all = time.perf_counter()
+    a = argparse.Namespace(**vars(args))
+    a.workload, a.memory_mode = "clip336", "patches"
+    model, opt = build(a, 0)
+    model.train()
+    images, di, tg = synthetic_batch(a.batch, a.seq_len, a.vocab, dev, 1000, model.encoder.image)
+
+    def step():
+        model.train_step(images, di, tg, next_images=images)
+        opt.step(5.0)
+
+    for _ in range(3):
+        step()
+    progs = [native.record(step) for _ in range(2)]
+    steps = max(2, args.also_steps)
     torch.cuda.synchronize()
-    K = max(1, args.steps // 4)
     t0 = time.perf_counter()
-    for _ in range(K):
-        ids = model.generate_batch(images, 2, never, max_len=args.max_len)
+    for i in range(steps):
+        opt._sync_lr()
+        progs[i % 2].run()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    toks = B * (args.max_len - 1) * K
-    out = {"metric": "greedy caption tokens/sec (batched KV-cache decode, 6L/d512 decoder + ViT-B/16)",
-           "value": round(toks / el, 1), "unit": "tokens/s", "n_gpus": 1, "steps": K, "warmup": max(1, args.warmup // 2),
-           "ms_per_step": round(1e3 * el / K, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": args.dtype, "data": "synthetic (randn 224x224 images; random-init weights)",
-           "config": {"workload": "configs[4]: inference.py greedy decode, cached cross-attn K/V, hipGraph-captured "
-                                  "per-token step", "images": B, "max_len": args.max_len, "memory_mode": "patches"},
-           "images_per_s": round(B * K / el, 2), "us_per_token_step": round(1e6 * el / K / (args.max_len - 1), 2),
-           "ids_per_caption": len(ids[0])}
-    print(json.dumps(out), flush=True)
+    fl = model.flops_per_pair(a.seq_len - 1)
+    v = a.batch * steps / el
+    out["configs[2]"] = {"metric": "image-caption pairs/sec (train step), 6L/d512 decoder + CLIP ViT-L/14@336",
+                         "value": round(v, 2), "unit": "pairs/s", "steps": steps, "ms_per_step": round(1e3 * el / steps, 3),
+                         "batch": a.batch, "seq_len": a.seq_len, "dtype": a.dtype,
+                         "step_mfma_frac": round(v * fl / (MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+                         "launch_path": "native replay (mit_plan_run)"}
+    del progs, model, opt, images, di, tg
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    d = decode_throughput(args)
+    g = decode_throughput(args, "graph")
+    out["configs[4]"] = dict(d, metric="greedy caption tokens/sec (batched KV-cache decode, 6L/d512 decoder + ViT-B/16)",
+                             note=DECODE_LAUNCH_NOTE, graph_tokens_per_s=g["value"],
+                             graph_us_per_token_step=g["us_per_token_step"])
+    out["seconds"] = round(time.perf_counter() - t_all, 1)
+    return out
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 with no launcher (WORLD_SIZE unset): start N rank processes of this script, one per
+    GPU, with the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+    MASTER_PORT). This parent makes no GPU call; rank 0 prints the JSON line. If a rank fails the
+    others are terminated and the failing status is returned."""
+    import socket
+    import subprocess
+    port = os.environ.get("MASTER_PORT")
+    if not port:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = str(sk.getsockname()[1])
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def main():
@@ -347,16 +457,24 @@ def main():
     ap.add_argument("--workload", default="train", choices=["train", "clip336", "cfg3", "decode"],
                     help="train: the BASELINE metric (default, configs[1]). clip336 / cfg3: the one-GPU share of "
                          "configs[2] / configs[3] (same step, CLIP-L encoders). decode: configs[4], batched greedy "
-                         "captioning (KV cache, hipGraph-replayed token step)")
+                         "captioning (KV cache, per-token step replayed as a native launch plan)")
     ap.add_argument("--decode-batch", type=int, default=256)
     ap.add_argument("--max-len", type=int, default=100, help="decode: ids per caption (config.MAX_SEQ_LEN)")
+    ap.add_argument("--also-steps", type=int, default=5, help="timed configs[2] steps in the `also` block")
+    ap.add_argument("--no-also", action="store_true",
+                    help="skip the `also` block (configs[2] train step and configs[4] decode in the same run, N=1)")
     args = ap.parse_args()
     if args.workload == "decode":
         return bench_decode(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
 
     from dist import DataParallel, init_from_env
     import torch.distributed as tdist
     rank, world = init_from_env()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
     if world == 1:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -481,6 +599,8 @@ def main():
                                  for k, v in agg.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "train":
         out["cpu_baseline"] = cpu_baseline(model, args)
+    if rank == 0 and world == 1 and not args.no_also and args.workload == "train":
+        out["also"] = also_block(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -240,10 +240,10 @@ __global__ void embed_decode_kernel(long B, long d, const int64_t* __restrict__ 
 // one block per row: first index of the maximum (torch.argmax), NaN counts as maximal
 __global__ __launch_bounds__(256) void greedy_pick_kernel(long V, const float* __restrict__ logits, long ld,
                                                           int64_t* __restrict__ ids, long ld_ids,
-                                                          const int64_t* __restrict__ pos, int64_t end_id,
+                                                          const int64_t* pos, int64_t end_id,
                                                           int64_t pad_id, int* __restrict__ finished,
                                                           int* __restrict__ n_finished, int* __restrict__ ticket,
-                                                          int64_t* __restrict__ pos_adv) {
+                                                          int64_t* pos_adv) {  // may alias pos: no __restrict__
   __shared__ float sv[4];
   __shared__ long si[4];
   const long b = blockIdx.x;
@@ -295,8 +295,11 @@ __global__ __launch_bounds__(256) void greedy_pick_kernel(long V, const float* _
         atomicAdd(n_finished, 1);
       }
     }
-    // position advance folded in (was its own launch): the ids store above consumed *pos, so when the
-    // last row's block takes the ticket every block has read the old position
+    // position advance folded in (was its own launch): every block has READ the old *pos before it
+    // takes a ticket -- the vmcnt(0) below retires this block's load of *pos (and its ids store)
+    // before the atomic issues, so the last ticket holder's write of the new position cannot
+    // overtake any block's read of the old one
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (ticket && atomicAdd(ticket, 1) == (int)gridDim.x - 1) {
       *pos_adv = p + 1;
       *ticket = 0;

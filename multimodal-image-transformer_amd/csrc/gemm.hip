@@ -56,7 +56,10 @@ struct Epi {
   int vec;  // 16-B vector epilogue legal (alignments / leading dims / N multiple of 8)
 };
 
-constexpr int ACT_RT = -1;  // activation read from Epi::act at run time (generic instance)
+constexpr int ACT_RT = -1;
+#ifndef MIT_G256_STORE  // gathered-epilogue store form (diagnostic builds only, tools/g256_stamps.py)
+#define MIT_G256_STORE 0
+#endif  // activation read from Epi::act at run time (generic instance)
 
 // FAST: bf16 vector epilogues use the branch-free GELU (gelu_fast, |err| ~1e-7, far below bf16
 // rounding); the scalar / fp32-parity path keeps ocml's erff
@@ -220,7 +223,13 @@ __device__ __forceinline__ void epi8x(const Epi& e, void* C, long ldc, long N, l
     bf16x8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+#if MIT_G256_STORE == 1  // diagnostic: non-temporal 16-B stores
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)((bf16*)C + r * ldc + c));
+#elif MIT_G256_STORE == 2  // diagnostic ONLY (wrong output): half the bytes, same store count
+    *(u32x2*)((bf16*)C + r * ldc + c) = u32x2{__builtin_bit_cast(u32x4, o)[0], __builtin_bit_cast(u32x4, o)[1]};
+#else
     *(bf16x8*)((bf16*)C + r * ldc + c) = o;
+#endif
   }
 }
 
@@ -714,6 +723,29 @@ __device__ __forceinline__ void bar_raw() {
 #define MIT_G256_PRIO 1
 #endif
 
+// Diagnostic build only (-DMIT_G256_STAMP, tools/g256_stamps.py): per workgroup, wave 0 and wave 4 stamp
+// the shader clock (s_memtime) at entry, after the prologue's first barrier, after the K loop and after
+// the epilogue's stores have drained, plus the 100 MHz global clock at entry / exit and the XCC id. The
+// stamps go to their own __device__ buffer (never an output); the shipped library compiles none of it.
+#ifdef MIT_G256_STAMP
+constexpr int G256_SLOTS = 16;  // wave 0: 0-5, wave 4: 6-11, 12 = exit global clock
+__device__ unsigned long long g256_stamp[16384 * G256_SLOTS];
+#define G256_STAMP(slot, val)                                                                        \
+  do {                                                                                               \
+    if (lane == 0 && (wid == 0 || wid == 4) && blockIdx.x < 16384)                                   \
+      g256_stamp[blockIdx.x * G256_SLOTS + (slot) + (wid == 4 ? 6 : 0)] = (unsigned long long)(val); \
+  } while (0)
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 15;
+}
+#else
+#define G256_STAMP(slot, val) \
+  do {                        \
+  } while (0)
+#endif
+
 // MI = 16-row MFMA blocks per wave in M: 8 (256-row tiles) or 5 / 6 (160 / 192-row tiles, K-contig A
 // with the register epilogue only): the N = 768 / 1024 encoder GEMMs (o-proj, fc2) have 150 / 580
 // 256-row tiles -- one round on 150 of 256 CUs, or a third round for 68 tiles -- and shorter tiles fill
@@ -727,6 +759,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   static_assert(MI == 8 || (MI >= 4 && MI < 8 && ALAY == MIT_K_CONTIG), "gemm256_kernel: short tiles need K-contig A");
+#ifdef MIT_G256_STAMP
+  G256_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  G256_STAMP(1, __builtin_amdgcn_s_memtime());
+  G256_STAMP(5, xcc_id());
+#endif
   constexpr int HR = 16 * MI;          // rows per wave group = rows per A half-tile
   constexpr int BMT = 2 * HR;          // tile rows
   constexpr int IH0 = (MI + 1) / 2;    // row blocks in the wave's first row half (ih = 0)
@@ -833,6 +870,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   wait_dma(issue(1, 0, 1));
   bar_raw();
   if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
+  G256_STAMP(2, __builtin_amdgcn_s_memtime());
 
 #if MIT_G256_PH4
   // 4 barriers per K-tile instead of 8: the same reads, DMA issues and waits in the same order,
@@ -951,6 +989,18 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   }
 #endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  G256_STAMP(3, __builtin_amdgcn_s_memtime());
+#ifdef MIT_G256_STAMP
+  struct StampEnd {  // stamps the epilogue's end (stores drained) on every return path
+    int lane, wid;
+    __device__ ~StampEnd() {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      G256_STAMP(4, __builtin_amdgcn_s_memtime());
+      if (wid == 0 && lane == 0 && blockIdx.x < 16384)
+        g256_stamp[blockIdx.x * G256_SLOTS + 12] = __builtin_amdgcn_s_memrealtime();
+    }
+  } stamp_end{lane, wid};
+#endif
   if (regepi) {
     // gathered register epilogue: v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane
     // group g with 8 consecutive columns: block 2jp + (g & 1), columns 8 * (g >> 1) .. +8
@@ -1847,3 +1897,16 @@ extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, const mit_ln_g
   }
   return MIT_OK;
 }
+
+#ifdef MIT_G256_STAMP
+// diagnostic build only: copy / clear the gemm256_kernel stamp buffer (tools/g256_stamps.py)
+extern "C" int mit_g256_stamps(unsigned long long* host, long n) {
+  const long cap = 16384L * G256_SLOTS;
+  if (n > cap) n = cap;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g256_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int mit_g256_stamps_clear() {
+  static unsigned long long zero[16384 * G256_SLOTS];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g256_stamp), zero, sizeof(zero), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+#endif

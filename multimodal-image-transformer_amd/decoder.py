@@ -796,7 +796,7 @@ class TransformerDecoder:
         tokens = tgt_tokens.to(self.device, torch.int64).contiguous()
         B, T = tokens.shape
         S = memory.shape[1]
-        self.store.ensure_shadow()
+        self.store.ensure_shadow(force=True)
         mem = memory.to(self.device, self.dtype).reshape(B * S, self.d).contiguous()
         keys = None
         if memory_padding_mask is not None:

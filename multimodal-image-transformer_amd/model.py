@@ -282,12 +282,13 @@ class ImageToTextModel:
         ev = self._enc_events.record(enc)
         self._prefetched = self._last_pf = (images, slot, out, ev)
 
-    def _encode_memory(self, images: torch.Tensor):
+    def _encode_memory(self, images: torch.Tensor, refresh: bool = True):
         """Returns (mem_rows, mem_ld, S, enc_rows, enc_ld): memory [B*S rows of d] and the
-        encoder features that feed the projection (for its weight gradient)."""
+        encoder features that feed the projection (for its weight gradient). refresh: re-cast the
+        bf16 weight shadow unconditionally (every path but the fused train step: params.ensure_shadow)."""
         B = images.shape[0]
         E, d = self.encoder.E, self.decoder_embed_dim
-        self.store.ensure_shadow()
+        self.store.ensure_shadow(force=refresh)
         self._gen += 1
         self._continue_prefetch()
         pf, self._prefetched = self._prefetched, None
@@ -412,7 +413,7 @@ class ImageToTextModel:
         tokens = decoder_input_tokens.to(self.device, torch.int64, non_blocking=True).contiguous()
         targets = target_tokens.to(self.device, torch.int64, non_blocking=True).contiguous()
         B, T = tokens.shape
-        mem, mem_ld, S, enc_rows, enc_ld = self._encode_memory(images)
+        mem, mem_ld, S, enc_rows, enc_ld = self._encode_memory(images, refresh=False)
         if next_images is not None:
             self.prefetch_encoder(next_images)
         dec = self.decoder
@@ -597,6 +598,13 @@ class ImageToTextModel:
         for stt in states:
             out.extend(stt.token_lists())
         return out
+
+    def sync_shadow(self):
+        """Re-cast the bf16 weight shadow the kernels read from the f32 master. Needed only after
+        editing weights out of band (through ``p.data``, which torch's version counter does not see)
+        and before a fused ``train_step``; every other path refreshes the shadow itself
+        (params.FlatParams.ensure_shadow)."""
+        self.store.sync_shadow()
 
     # --- checkpoints (reference key names, SURVEY.md §8b) --------------------------------------
     def state_dict(self) -> Dict[str, torch.Tensor]:

@@ -14,6 +14,7 @@ import os
 from typing import Optional
 
 import torch
+from torch.utils._python_dispatch import TorchDispatchMode
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MIT_HIP_LIB", os.path.join(_HERE, "lib", "libmit_hip.so"))
@@ -189,6 +190,36 @@ class on_stream:
         _stream_override = self.prev
 
 
+_hip_rt = None
+
+
+def hip_runtime() -> ctypes.CDLL:
+    """The HIP runtime library this process already uses (torch's, or the one libmit_hip.so links):
+    the libamdhip64 mapped into the process (/proc/self/maps), else the first of the usual sonames
+    that loads -- never a second runtime of another ROCm major version."""
+    global _hip_rt
+    if _hip_rt is not None:
+        return _hip_rt
+    load_library()  # maps the runtime libmit_hip.so was linked against
+    paths = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if parts and "libamdhip64.so" in parts[-1] and parts[-1] not in paths:
+                    paths.append(parts[-1])
+    except OSError:
+        pass
+    errs = []
+    for name in paths + ["libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"]:
+        try:
+            _hip_rt = ctypes.CDLL(name)
+            return _hip_rt
+        except OSError as e:
+            errs.append(str(e))
+    raise NativeError("cannot load the HIP runtime (libamdhip64): " + "; ".join(errs))
+
+
 class HipEvents:
     """Timing-free HIP events from a recycled pool, recorded / waited on raw stream pointers
     (cross-stream edges of the step without torch.cuda.Event's Python overhead). Record and wait go
@@ -198,7 +229,7 @@ class HipEvents:
 
     def __init__(self, n=64):
         if HipEvents._hip is None:
-            h = ctypes.CDLL("libamdhip64.so.7")  # the runtime torch already loaded
+            h = hip_runtime()
             h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(vp), ctypes.c_uint]
             h.hipEventDestroy.argtypes = [vp]
             HipEvents._hip = h
@@ -262,10 +293,39 @@ class Program:
 
 
 _recording: Optional[Program] = None
+_guard_paused = 0
+
+
+class _NoTorchKernels(TorchDispatchMode):
+    """Active while native.record() runs fn(): a replay re-issues only the recorded NATIVE launches,
+    so a torch op that would enqueue GPU work (a fill_, copy_, arithmetic on a CUDA tensor) would be
+    silently dropped from every replay. Any such op raises instead. Metadata-only ops (views,
+    reshapes, size queries, empty allocations) and ops on CPU tensors pass; host_call() actions (DP
+    collectives, callbacks), which are recorded and re-run on replay, are exempt.
+    MIT_RECORD_GUARD=0 switches the check off."""
+    ALLOWED = {"view", "_unsafe_view", "as_strided", "slice", "select", "narrow", "reshape", "alias", "detach",
+               "t", "transpose", "permute", "unsqueeze", "squeeze", "expand", "split", "split_with_sizes",
+               "chunk", "unbind", "flatten", "contiguous", "empty", "empty_like", "empty_strided", "view_as",
+               "_reshape_alias", "lift_fresh", "sym_size", "sym_stride", "sym_numel", "sym_storage_offset",
+               "is_same_size", "_local_scalar_dense", "item", "_to_copy", "to", "record_stream", "set_"}
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        name = func.__name__.split(".")[0]
+        if not _guard_paused and name not in self.ALLOWED:
+            def on_gpu(x):
+                return isinstance(x, torch.Tensor) and x.is_cuda
+            flat = list(args) + list(kwargs.values())
+            if any(on_gpu(x) or (isinstance(x, (list, tuple)) and any(on_gpu(y) for y in x)) for x in flat):
+                raise NativeError(f"native.record: torch op {func} would enqueue GPU work while recording; a "
+                                  f"replay re-issues only native launches and would drop it (do it outside the "
+                                  f"recorded function, or through a native entry point / host_call)")
+        return func(*args, **kwargs)
 
 
 def record(fn) -> Program:
-    """Run fn() once for real while recording every native launch (and host_call) into a Program."""
+    """Run fn() once for real while recording every native launch (and host_call) into a Program.
+    A torch op on a CUDA tensor inside fn() raises (see _NoTorchKernels)."""
     global _recording
     if _recording is not None:
         raise NativeError("record: already recording")
@@ -273,8 +333,13 @@ def record(fn) -> Program:
     if not lib().mit_plan_begin():
         raise NativeError(f"mit_plan_begin failed: {lib().mit_last_error().decode()}")
     _recording = prog
+    guard = os.environ.get("MIT_RECORD_GUARD", "1") != "0"
     try:
-        fn()
+        if guard:
+            with _NoTorchKernels():
+                fn()
+        else:
+            fn()
     finally:
         prog.items.append((0, lib().mit_plan_end()))
         _recording = None
@@ -284,12 +349,15 @@ def record(fn) -> Program:
 def host_call(fn):
     """Run a host-side action now; inside record(), also record it as a host step of the Program
     between two native plans (so a replay re-runs it at the same point of the launch sequence)."""
+    global _guard_paused
     if _recording is not None:
         _recording.items.append((0, lib().mit_plan_end()))
         _recording.items.append((1, fn))
+        _guard_paused += 1
         try:
             fn()
         finally:
+            _guard_paused -= 1
             if not lib().mit_plan_begin():
                 raise NativeError(f"mit_plan_begin failed: {lib().mit_last_error().decode()}")
         return

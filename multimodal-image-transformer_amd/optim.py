@@ -75,6 +75,85 @@ def _store_of(params) -> FlatParams:
     return st
 
 
+def reference_state(store: FlatParams, lay: dict, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, step: int,
+                    group: dict) -> dict:
+    """torch.optim.AdamW state_dict of the REFERENCE model's parameters (frozen encoder indices first,
+    then reference_trainable order) from flat moment buffers laid out like ``store``."""
+    from decoder import flat_to_reference
+    names = reference_trainable(lay)
+    base = lay["n_encoder_params"]
+    ref = {}
+    for key, buf in (("exp_avg", exp_avg), ("exp_avg_sq", exp_avg_sq)):
+        view = _BufView(store, buf)
+        sd = flat_to_reference(view, lay["L"], lay["d"])
+        if lay.get("proj_in") is not None:
+            sd["projection.weight"] = view.p("projection.weight").detach().clone()
+            sd["projection.bias"] = view.p("projection.bias").detach().clone()
+        ref[key] = sd
+    state = {}
+    if step > 0:
+        for i, (n, _) in enumerate(names):
+            state[base + i] = {"step": torch.tensor(float(step)), "exp_avg": ref["exp_avg"][n].cpu(),
+                               "exp_avg_sq": ref["exp_avg_sq"][n].cpu()}
+    g = {"lr": float(group["lr"]), "betas": tuple(group["betas"]), "eps": group["eps"],
+         "weight_decay": group["weight_decay"]}
+    g.update(amsgrad=False, maximize=False, foreach=None, capturable=False, differentiable=False, fused=None,
+             decoupled_weight_decay=True, params=list(range(base + len(names))))
+    return {"state": state, "param_groups": [g]}
+
+
+def flat_moments(store: FlatParams, lay: dict, sd: dict):
+    """Validate a torch.optim.AdamW state_dict of the reference model and convert it -> (exp_avg,
+    exp_avg_sq) flat f32 buffers laid out like ``store`` (on its device), the step count, and the
+    parameter group. Raises OptimizerStateError before anything is written anywhere."""
+    from decoder import reference_to_flat
+    if not isinstance(sd, dict) or "state" not in sd or "param_groups" not in sd:
+        raise OptimizerStateError(f"not a torch.optim.AdamW state_dict (keys: {sorted(sd) if isinstance(sd, dict) else type(sd)})")
+    names = reference_trainable(lay)
+    groups = sd["param_groups"]
+    if len(groups) != 1:
+        raise OptimizerStateError(f"{len(groups)} parameter groups; the reference builds one (train.py:319-325)")
+    g0 = groups[0]
+    if g0.get("amsgrad") or g0.get("maximize"):
+        raise OptimizerStateError("amsgrad / maximize AdamW states are not supported")
+    idx = list(g0["params"])
+    if len(idx) < len(names):
+        raise OptimizerStateError(f"the state covers {len(idx)} parameters, the model trains {len(names)}")
+    train_idx = idx[len(idx) - len(names):]
+    frozen_with_state = [i for i in idx[:len(idx) - len(names)] if i in sd["state"]]
+    if frozen_with_state:
+        raise OptimizerStateError(f"optimizer state for {len(frozen_with_state)} parameters that are frozen here "
+                                  f"(encoder / layout mismatch)")
+    steps = set()
+    moments = {"exp_avg": {}, "exp_avg_sq": {}}
+    for i, (n, shape) in zip(train_idx, names):
+        s = sd["state"].get(i)
+        if s is None:  # never stepped (no gradient yet): zero moments
+            for k in moments:
+                moments[k][n] = torch.zeros(shape)
+            continue
+        for k in moments:
+            t = s.get(k)
+            if t is None or tuple(t.shape) != tuple(shape):
+                raise OptimizerStateError(f"{n}: {k} has shape {None if t is None else tuple(t.shape)}, "
+                                          f"expected {tuple(shape)}")
+            moments[k][n] = t.detach().float().cpu()
+        steps.add(float(s["step"]))
+    if len(steps) > 1:
+        raise OptimizerStateError(f"per-parameter step counts differ ({sorted(steps)[:4]}); the flat layout "
+                                  f"fuses tensors and keeps one step count")
+    out = []
+    for k in ("exp_avg", "exp_avg_sq"):
+        flat = reference_to_flat(moments[k], lay["L"], lay["d"])
+        buf = torch.zeros(store.numel, dtype=torch.float32, device=store.device)
+        view = _BufView(store, buf)
+        for n, t in flat.items():
+            dst = view.p(n)
+            dst[:t.shape[0]].copy_(t.to(dst.device).reshape((t.shape[0],) + tuple(dst.shape[1:])))
+        out.append(buf)
+    return out[0], out[1], int(round(steps.pop())) if steps else 0, g0
+
+
 class AdamW:
     def __init__(self, params, lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-5):
         store = _store_of(params)
@@ -116,78 +195,17 @@ class AdamW:
         return lay
 
     def state_dict(self) -> dict:
-        from decoder import flat_to_reference
-        lay = self._layout()
-        names = reference_trainable(lay)
-        base = lay["n_encoder_params"]
-        step = float(int(self.step_t.item()))
-        ref = {}
-        for key, buf in (("exp_avg", self.store.exp_avg), ("exp_avg_sq", self.store.exp_avg_sq)):
-            sd = flat_to_reference(_BufView(self.store, buf), lay["L"], lay["d"])
-            if lay.get("proj_in") is not None:
-                sd["projection.weight"] = _BufView(self.store, buf).p("projection.weight").detach().clone()
-                sd["projection.bias"] = _BufView(self.store, buf).p("projection.bias").detach().clone()
-            ref[key] = sd
-        state = {}
-        if step > 0:
-            for i, (n, _) in enumerate(names):
-                state[base + i] = {"step": torch.tensor(step), "exp_avg": ref["exp_avg"][n].cpu(),
-                                   "exp_avg_sq": ref["exp_avg_sq"][n].cpu()}
-        g = dict(self.param_groups[0])
-        g.update(amsgrad=False, maximize=False, foreach=None, capturable=False, differentiable=False, fused=None,
-                 decoupled_weight_decay=True, params=list(range(base + len(names))))
-        return {"state": state, "param_groups": [g]}
+        return reference_state(self.store, self._layout(), self.store.exp_avg, self.store.exp_avg_sq,
+                               int(self.step_t.item()), self.param_groups[0])
 
     def load_state_dict(self, sd: dict):
         """torch.optim.AdamW state (reference checkpoints, or ours) -> the flat moments, the step
         count and the hyper-parameters. Validated completely before anything is written."""
-        from decoder import reference_to_flat
-        if not isinstance(sd, dict) or "state" not in sd or "param_groups" not in sd:
-            raise OptimizerStateError(f"not a torch.optim.AdamW state_dict (keys: {sorted(sd) if isinstance(sd, dict) else type(sd)})")
-        lay = self._layout()
-        names = reference_trainable(lay)
-        groups = sd["param_groups"]
-        if len(groups) != 1:
-            raise OptimizerStateError(f"{len(groups)} parameter groups; the reference builds one (train.py:319-325)")
-        g0 = groups[0]
-        if g0.get("amsgrad") or g0.get("maximize"):
-            raise OptimizerStateError("amsgrad / maximize AdamW states are not supported")
-        idx = list(g0["params"])
-        if len(idx) < len(names):
-            raise OptimizerStateError(f"the state covers {len(idx)} parameters, the model trains {len(names)}")
-        train_idx = idx[len(idx) - len(names):]
-        frozen_with_state = [i for i in idx[:len(idx) - len(names)] if i in sd["state"]]
-        if frozen_with_state:
-            raise OptimizerStateError(f"optimizer state for {len(frozen_with_state)} parameters that are frozen here "
-                                      f"(encoder / layout mismatch)")
-        steps = set()
-        moments = {"exp_avg": {}, "exp_avg_sq": {}}
-        for i, (n, shape) in zip(train_idx, names):
-            s = sd["state"].get(i)
-            if s is None:  # never stepped (no gradient yet): zero moments
-                for k in moments:
-                    moments[k][n] = torch.zeros(shape)
-                continue
-            for k in moments:
-                t = s.get(k)
-                if t is None or tuple(t.shape) != tuple(shape):
-                    raise OptimizerStateError(f"{n}: {k} has shape {None if t is None else tuple(t.shape)}, "
-                                              f"expected {tuple(shape)}")
-                moments[k][n] = t.detach().float().cpu()
-            steps.add(float(s["step"]))
-        if len(steps) > 1:
-            raise OptimizerStateError(f"per-parameter step counts differ ({sorted(steps)[:4]}); the fused AdamW "
-                                      f"keeps one step count")
-        # validated: write
-        for k, buf in (("exp_avg", self.store.exp_avg), ("exp_avg_sq", self.store.exp_avg_sq)):
-            flat = reference_to_flat(moments[k], lay["L"], lay["d"])
-            view = _BufView(self.store, buf)
-            with torch.no_grad():
-                buf.zero_()
-                for n, t in flat.items():
-                    dst = view.p(n)
-                    dst[:t.shape[0]].copy_(t.to(dst.device).reshape((t.shape[0],) + tuple(dst.shape[1:])))
-        self.step_t.fill_(int(round(steps.pop())) if steps else 0)
+        ea, eas, step, g0 = flat_moments(self.store, self._layout(), sd)
+        with torch.no_grad():
+            self.store.exp_avg.copy_(ea)
+            self.store.exp_avg_sq.copy_(eas)
+        self.step_t.fill_(step)
         self.betas = tuple(g0.get("betas", self.betas))
         self.eps = g0.get("eps", self.eps)
         self.weight_decay = g0.get("weight_decay", self.weight_decay)

@@ -75,12 +75,17 @@ class FlatParams:
             native.cast_f32(self.master, self.shadow)
         self._synced = self.master._version
 
-    def ensure_shadow(self):
-        """Refresh the bf16 shadow if the f32 master was modified by torch since the last sync: an
-        in-place update through a parameter view (torch.optim.AdamW.step, p.data.copy_, ...) bumps
-        the version counter the views share with the master. The fused optim.AdamW writes master
-        and shadow in one kernel (no version bump, nothing to do)."""
-        if self.shadow is not self.master and self.master._version != self._synced:
+    def ensure_shadow(self, force: bool = False):
+        """Refresh the bf16 shadow from the f32 master. Without ``force`` only when torch modified the
+        master through a parameter view since the last sync (in-place ops on the views, e.g.
+        torch.optim.AdamW.step, bump the version counter they share with the master); the fused
+        optim.AdamW writes master and shadow in one kernel (no bump, nothing to do). An edit through
+        ``p.data`` (``p.data.copy_``, ...) is NOT seen by the version counter (``.data`` is a detached
+        alias with its own counter): the non-fused paths (autograd forward, evaluation, generation)
+        therefore refresh with ``force=True`` every call (one 1.5-byte-per-parameter cast), and the
+        fused train step -- which checks the counter only -- needs ``model.sync_shadow()`` after such
+        an out-of-band edit."""
+        if self.shadow is not self.master and (force or self.master._version != self._synced):
             self.sync_shadow()
 
     def zero_grad(self):

@@ -167,14 +167,84 @@ def synthetic_loader(n_batches, B, seq_len, vocab, image, seed=0):
     return out
 
 
+def _torch_adamw_params(model, optimizer):
+    """(name, parameter) of a torch.optim.AdamW built over model.parameters() (one group, the flat
+    entries in order); raises CheckpointError for any other parameter list."""
+    named = list(model.named_parameters())
+    g = optimizer.param_groups
+    if len(g) != 1 or len(g[0]["params"]) != len(named) or any(a is not b for a, (_, b) in zip(g[0]["params"], named)):
+        raise CheckpointError("checkpoints hold the reference's optimizer layout: the torch.optim.AdamW must be built "
+                              "over model.parameters() as one parameter group (train.py:319-325)")
+    return named
+
+
+def optimizer_state_reference(model, optimizer) -> dict:
+    """The optimizer's state in the REFERENCE checkpoint format: torch.optim.AdamW's state_dict with
+    the reference model's parameter indices (frozen encoder first, then projection + decoder in the
+    reference's tensors, train.py:422-436). optim.AdamW writes it itself; a torch.optim.AdamW over
+    model.parameters() (the flat, fused entries: layers.i.cross_kv, self_in, padded fc_out, ...)
+    is converted through the same flat -> reference mapping."""
+    if isinstance(optimizer, optim.AdamW):
+        return optimizer.state_dict()
+    if not isinstance(optimizer, torch.optim.AdamW):
+        raise CheckpointError(f"save_checkpoint: {type(optimizer).__name__} has no reference-format state "
+                              f"(optim.AdamW or torch.optim.AdamW over model.parameters())")
+    named = _torch_adamw_params(model, optimizer)
+    store = model.store
+    ea = torch.zeros(store.numel, dtype=torch.float32, device=store.device)
+    eas = torch.zeros_like(ea)
+    steps = set()
+    with torch.no_grad():
+        for n, p in named:
+            st = optimizer.state.get(p)
+            if not st:
+                continue
+            _, off, k = store.index[n]
+            ea[off:off + k].copy_(st["exp_avg"].reshape(-1))
+            eas[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+            steps.add(float(st["step"]))
+    if len(steps) > 1:
+        raise CheckpointError(f"per-parameter step counts differ ({sorted(steps)[:4]}): not representable in the "
+                              f"reference layout, whose tensors the flat entries fuse")
+    step = int(round(steps.pop())) if steps else 0
+    return optim.reference_state(store, store.layout, ea, eas, step, optimizer.param_groups[0])
+
+
+def load_optimizer_state_reference(model, optimizer, sd: dict):
+    """Inverse of optimizer_state_reference: a reference-format AdamW state -> optim.AdamW, or -> a
+    torch.optim.AdamW over model.parameters() (its per-parameter state for the flat entries).
+    Validated completely before anything is written."""
+    if isinstance(optimizer, optim.AdamW):
+        return optimizer.load_state_dict(sd)
+    if not isinstance(optimizer, torch.optim.AdamW):
+        raise CheckpointError(f"load_checkpoint: {type(optimizer).__name__} cannot take a reference-format "
+                              f"AdamW state (optim.AdamW or torch.optim.AdamW over model.parameters())")
+    named = _torch_adamw_params(model, optimizer)
+    store = model.store
+    ea, eas, step, g0 = optim.flat_moments(store, store.layout, sd)
+    for n, p in named:
+        _, off, k = store.index[n]
+        if step > 0:
+            optimizer.state[p] = {"step": torch.tensor(float(step)),
+                                  "exp_avg": ea[off:off + k].view(p.shape).clone(),
+                                  "exp_avg_sq": eas[off:off + k].view(p.shape).clone()}
+        else:
+            optimizer.state.pop(p, None)
+    grp = optimizer.param_groups[0]
+    for key in ("lr", "betas", "eps", "weight_decay"):
+        if key in g0:
+            grp[key] = tuple(g0[key]) if key == "betas" else g0[key]
+
+
 def save_checkpoint(model, optimizer, epoch, val_loss, path_prefix, scheduler=None):
     """train.py:412-442: a .pt dict {epoch, model_state_dict, optimizer_state_dict,
     scheduler_state_dict, best_val_loss} and a .safetensors of model.state_dict() (reference key
-    names)."""
+    names). The optimizer state is always in the reference's format (optimizer_state_reference),
+    so the reference resumes it and vice versa, for optim.AdamW and torch.optim.AdamW alike."""
     from safetensors.torch import save_file
     name = f"{path_prefix}_{config.ENCODER_MODEL_NAME.replace('/', '_')}_epoch_{epoch + 1}_val_loss_{val_loss:.4f}"
     sd = {k: v.detach().cpu().contiguous() for k, v in model.state_dict().items()}
-    torch.save({"epoch": epoch, "model_state_dict": sd, "optimizer_state_dict": optimizer.state_dict(),
+    torch.save({"epoch": epoch, "model_state_dict": sd, "optimizer_state_dict": optimizer_state_reference(model, optimizer),
                 "scheduler_state_dict": scheduler.state_dict() if scheduler is not None else None,
                 "best_val_loss": val_loss}, name + ".pt")
     save_file(sd, name + ".safetensors")
@@ -194,8 +264,9 @@ def load_checkpoint(model, optimizer, scheduler, path):
     not the optimizer — a silent half-resume this build refuses.
     Loaded with torch.load(weights_only=True): tensors and plain containers only, nothing in the
     file is executed (the reference uses weights_only=False). A .safetensors path
-    (inference.py:66-67) restores the model weights only. The optimizer state may be torch.optim
-    .AdamW's (the reference's, or optim.AdamW's, which writes the same format)."""
+    (inference.py:66-67) restores the model weights only. The optimizer state is torch.optim.AdamW's
+    over the REFERENCE model's parameters (the reference's checkpoints, and save_checkpoint's); it
+    resumes optim.AdamW or a torch.optim.AdamW built over model.parameters()."""
     if not path or not os.path.exists(path):
         if path:
             print(f"Warning: checkpoint '{path}' does not exist. Starting training from scratch.")
@@ -212,8 +283,9 @@ def load_checkpoint(model, optimizer, scheduler, path):
             if k not in ck:
                 raise KeyError(f"checkpoint has no '{k}' (keys: {sorted(ck)})")
         model.check_state_dict(ck["model_state_dict"])
-        # optim.AdamW.load_state_dict validates everything before it writes (all or nothing)
-        optimizer.load_state_dict(ck["optimizer_state_dict"])
+        # validates everything before it writes (all or nothing), for optim.AdamW and for a
+        # torch.optim.AdamW over model.parameters()
+        load_optimizer_state_reference(model, optimizer, ck["optimizer_state_dict"])
     except Exception as e:  # noqa: BLE001
         raise CheckpointError(f"cannot resume from '{path}': {e}") from e
     model.load_state_dict(ck["model_state_dict"])
@@ -224,16 +296,36 @@ def load_checkpoint(model, optimizer, scheduler, path):
     return start, ck.get("best_val_loss", math.inf)
 
 
+def shard_batches(batches, rank: int, world: int):
+    """The rank's share of every global batch: rows [rank*B/world, (rank+1)*B/world) (the
+    data-parallel loader; each global batch of B pairs is split evenly over the ranks)."""
+    for b in batches:
+        B = b["decoder_input_tokens"].shape[0]
+        if B % world:
+            raise ValueError(f"global batch {B} is not divisible by the {world} data-parallel ranks")
+        lo, hi = rank * B // world, (rank + 1) * B // world
+        yield {k: v[lo:hi] for k, v in b.items()}
+
+
 def main(argv=None):
+    """train.py:282-452 on synthetic batches. Data parallel when launched with WORLD_SIZE > 1
+    (torchrun, one process per GPU; RCCL): every rank takes its slice of each global batch of
+    --batch-size pairs (shard_batches), the decoder gradients are all-reduced by bucket during the
+    backward (dist.DataParallel) with the loss normalised by the GLOBAL non-PAD count, so the step
+    equals the single-process step at the global batch; validation runs the whole batch on every
+    rank (identical results), and only rank 0 writes checkpoints. Returns the per-epoch
+    (train, val) losses."""
     ap = argparse.ArgumentParser(description="Train the captioning model on synthetic batches (MI355X path)")
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--batches", type=int, default=20)
-    ap.add_argument("--batch-size", type=int, default=config.BATCH_SIZE)
+    ap.add_argument("--batch-size", type=int, default=config.BATCH_SIZE, help="global batch (all ranks)")
     ap.add_argument("--seq-len", type=int, default=64)
     ap.add_argument("--out", default=None, help="checkpoint prefix (optional)")
     ap.add_argument("--resume", default=getattr(config, "RESUME_CHECKPOINT_PATH", None),
                     help="resume from a .pt checkpoint (train.py:343-375)")
     args = ap.parse_args(argv)
+    from dist import DataParallel, init_from_env
+    rank, world = init_from_env()
     torch.manual_seed(config.RANDOM_SEED)
     model = ImageToTextModel(config.VOCAB_SIZE, config.DECODER_EMBED_DIM, config.DECODER_HEADS, config.DECODER_LAYERS,
                              config.DECODER_FF_DIM, config.MAX_SEQ_LEN, config.DECODER_DROPOUT, config.PAD_TOKEN_ID)
@@ -245,15 +337,27 @@ def main(argv=None):
     train = synthetic_loader(args.batches, args.batch_size, args.seq_len, config.VOCAB_SIZE, model.encoder.image, 1)
     val = synthetic_loader(2, args.batch_size, args.seq_len, config.VOCAB_SIZE, model.encoder.image, 2)
     start, best = load_checkpoint(model, opt, sched, args.resume)
+    dp = None
+    if world > 1:
+        import torch.distributed as tdist
+        dp = DataParallel(model)  # broadcasts rank 0's weights (a resumed state is identical on every rank)
+        train = list(shard_batches(train, rank, world))
+    history = []
     for epoch in range(start, args.epochs):
         t0 = time.time()
-        tl = train_one_epoch(model, train, opt, None, "cuda", config.GRAD_CLIP_VALUE, sched, epoch, config.LOG_INTERVAL,
-                             None)
+        tl = train_one_epoch(model, train, opt, None, "cuda", config.GRAD_CLIP_VALUE, sched, epoch,
+                             config.LOG_INTERVAL if rank == 0 else 0, None, dist=dp)
         vl = evaluate(model, val, None, "cuda")
-        print(f"epoch {epoch + 1}: train {tl:.4f} val {vl:.4f} ({time.time() - t0:.1f}s)", flush=True)
+        history.append((tl, vl))
+        if rank == 0:
+            print(f"epoch {epoch + 1}: train {tl:.4f} val {vl:.4f} ({time.time() - t0:.1f}s, {world} rank(s))", flush=True)
         if vl < best and args.out:
             best = vl
-            print("saved", save_checkpoint(model, opt, epoch, vl, args.out, sched))
+            if rank == 0:
+                print("saved", save_checkpoint(model, opt, epoch, vl, args.out, sched))
+            if world > 1:
+                tdist.barrier()
+    return history
 
 
 if __name__ == "__main__":

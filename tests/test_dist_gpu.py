@@ -102,3 +102,77 @@ def test_dp2_train_step_on_hip_path_matches_reference():
     for k in FX.trainable_names(meta):
         FX.compare_stat("grad1", k, named[k] * coef, T, meta, rtol=2e-3, atol=2e-6, scale_tol=1e-3, outlier_frac=2e-3)
         FX.compare_stat("delta1", k, deltas[k], T, meta, rtol=2e-3, atol=2e-6)
+
+
+def _train_main_worker(rank, world, port, q):
+    """train.main on 2 synthetic global batches of 8 pairs (dropout off): world 1 = one process with
+    the whole batch, world 2 = two gloo ranks on cuda:0 with their halves (shard_batches)."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "..", "multimodal-image-transformer_amd"))
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                          WORLD_SIZE=str(world), MIT_DIST_BACKEND="gloo")
+    else:
+        os.environ.pop("WORLD_SIZE", None)
+    torch.cuda.set_device(0)
+    import config
+    config.DECODER_DROPOUT = 0.0
+    config.WARMUP_STEPS = 0
+    config.LOG_INTERVAL = 0
+    import train
+    hist = train.main(["--batches", "2", "--batch-size", "8", "--seq-len", "16", "--epochs", "1"])
+    if rank == 0:
+        q.put(hist)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def _run_train_main(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_main_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    hist = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return hist
+
+
+def test_train_main_dp2_matches_one_rank_global_batch():
+    """train.main (reference train.py:62-123 loop, its main's DP wiring): 2 ranks x half batches give
+    the 1-rank global-batch epoch losses (train mean over the 2 batches, then validation after the
+    updates). bf16 GEMMs on different M sum in different orders: 2e-3 relative."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    one = _run_train_main(1)
+    two = _run_train_main(2)
+    assert len(one) == len(two) == 1
+    (t1, v1), (t2, v2) = one[0], two[0]
+    assert abs(t1 - t2) <= 2e-3 * abs(t1), (t1, t2)
+    assert abs(v1 - v2) <= 2e-3 * abs(v1), (v1, v2)
+
+
+def test_bench_spawns_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher starts its 2 rank processes itself (gloo here: one GPU);
+    the JSON line reports n_gpus 2 and the whole-job pairs/s."""
+    import json
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MIT_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--batch", "8", "--no-cpu-baseline", "--no-roofline", "--no-also"],
+                       env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 16 and rec["value"] > 0

@@ -15,7 +15,7 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("dW kv_all", 6144, 512, 12608, 1, 1), ("dX kv_all", 12608, 512, 6144, 0, 1), ("dW ffn1", 2048, 512, 4032, 1, 1),
     ("4096^3", 4096, 4096, 4096, 0, 0),
     ("enc fc1+gelu", 12608, 3072, 768, 0, 0, "gelu"), ("enc fc2+res", 12608, 768, 3072, 0, 0, "res"),
-    ("enc qkv+bias", 12608, 2304, 768, 0, 0, "bias"), ("dec ffn1+relu+drop", 4032, 2048, 512, 0, 0, "reludrop"),
+    ("enc qkv+bias", 12608, 2304, 768, 0, 0, "bias"), ("enc o+res", 12608, 768, 768, 0, 0, "res"), ("dec ffn1+relu+drop", 4032, 2048, 512, 0, 0, "reludrop"),
     # the d_model = 512 decoder GEMMs (128 output tiles)
     ("fwd out+bias", 4032, 512, 512, 0, 0, "bias"), ("fwd lin2+res", 4032, 512, 2048, 0, 0, "res"),
     ("dX out", 4032, 512, 512, 0, 1), ("dX q+res", 4032, 512, 512, 0, 1, "res0"),
@@ -26,6 +26,9 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("clip o+res", 36928, 1024, 1024, 0, 0, "res"), ("clip fc2+res", 36928, 1024, 4096, 0, 0, "res"),
     ("clip qkv", 36928, 3072, 1024, 0, 0, "bias"), ("clip fc1+gelu", 36928, 4096, 1024, 0, 0, "gelu"),
     ("cfg3 o+res", 16448, 1024, 1024, 0, 0, "res"), ("cfg3 fc2+res", 16448, 1024, 4096, 0, 0, "res"),
+    # epilogue-concurrency probes (tools/g256_stamps.py): 8 / 64 / 128 tiles of the encoder's K = 768
+    ("iso8", 2048, 256, 768, 0, 0), ("iso8 res", 2048, 256, 768, 0, 0, "res"), ("iso64", 2048, 2048, 768, 0, 0),
+    ("iso128", 4096, 2048, 768, 0, 0),
 ]
 
 
