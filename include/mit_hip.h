@@ -152,6 +152,20 @@ int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x, long ldx, 
                       float r_drop_p, const uint64_t* seed, uint32_t site, const float* gamma, const float* beta,
                       float eps, void* z, void* y, long ldy, float* mean, float* rstd, void* stream);
 
+/* The encoder's f32 residual stream (encoder.py, as torch.autocast keeps HF ViT/CLIP's residual
+ * adds: modeling_vit.py:312-323, modeling_clip.py:379-393): z = x + r, y = LN(z).
+ *   x f32 [rows, ldx]; r = the sublayer's bf16 output (NULL: z = x); z f32 [rows, cols] (NULL: not
+ *   written; may alias x; needs ldx == cols); y in y_dtype (MIT_BF16: the next GEMM's operand; MIT_F32: a new
+ *   f32 stream, CLIP's pre_layrnorm). cols % 8 == 0, cols <= 1024, leading dims % 8 == 0, 16-B
+ *   aligned pointers, y aliases neither x nor r. Replaces the same nn.LayerNorm calls as
+ *   mit_layernorm_fwd (modeling_vit.py:274,281,385; modeling_clip.py:358,360,642). */
+int mit_layernorm_fwd_x32(long rows, long cols, const float* x, long ldx, const void* r, long ldr, float* z,
+                          const float* gamma, const float* beta, float eps, void* y, int y_dtype, long ldy, void* stream);
+/* y (bf16) = x + r: the last residual add of the f32 stream, rounded for the encoder's consumers
+ * (CLIP's last_hidden_state, modeling_clip.py:649, has no final LayerNorm). r may be NULL. */
+int mit_residual_out(long rows, long cols, const float* x, long ldx, const void* r, long ldr, void* y, long ldy,
+                     void* stream);
+
 /* Backward of y = LN(z), z = x + dropout(r):
  *   dx = dz = dLN(dy) (dx may alias dy), dr = dz * dropout_mask (may be NULL)
  *   dgamma/dbeta: f32 [cols], overwritten. Both NULL: the per-block column partials are left in

@@ -76,6 +76,10 @@ DTYPE = os.environ.get("MIT_DTYPE", "bf16")
 # Local weights for the frozen encoder (HF state_dict names, .safetensors). There is no network, so
 # from_pretrained(ENCODER_MODEL_NAME) is replaced by this file; None -> seeded random init.
 ENCODER_WEIGHTS_PATH = os.environ.get("MIT_ENCODER_WEIGHTS", None)
+# bf16 encoders: keep the residual stream in f32 (as torch.autocast does; the sublayer outputs stay
+# bf16). "auto" = the 24-layer CLIP-L towers (configs[2] / configs[3]), where a bf16 stream doubles
+# the encoder's error; "on" / "off" force it.
+ENCODER_F32_RESIDUAL = os.environ.get("MIT_ENCODER_F32_RESIDUAL", "auto")
 
 # Encoder geometry by model name (values of the HF configs the names resolve to).
 ENCODER_SPECS = {

@@ -722,13 +722,24 @@ __device__ __forceinline__ void bar_raw() {
 #ifndef MIT_G256_PRIO  // raise the wave priority around each MFMA block
 #define MIT_G256_PRIO 1
 #endif
+// Epilogue staged through LDS (f32, two passes of 128 tile rows) so that every store instruction
+// writes MIT_G256_EPR whole rows of the tile (2: two 512-B row runs per wave instruction). The
+// register epilogue's stores (16 rows x 64 B per instruction) and the 8-rows x 128-B form both run
+// at ~30 GB/s per CU (4.4-5 us per 256x256 bf16 tile, tools/g256_stamps.py), ~4x slower than
+// long contiguous runs: the store INSTRUCTION pattern, not bytes, bounds the epilogue.
+#ifndef MIT_G256_EPI_LDS
+#define MIT_G256_EPI_LDS 1
+#endif
+#ifndef MIT_G256_EPR
+#define MIT_G256_EPR 2
+#endif
 
 // Diagnostic build only (-DMIT_G256_STAMP, tools/g256_stamps.py): per workgroup, wave 0 and wave 4 stamp
 // the shader clock (s_memtime) at entry, after the prologue's first barrier, after the K loop and after
 // the epilogue's stores have drained, plus the 100 MHz global clock at entry / exit and the XCC id. The
 // stamps go to their own __device__ buffer (never an output); the shipped library compiles none of it.
 #ifdef MIT_G256_STAMP
-constexpr int G256_SLOTS = 16;  // wave 0: 0-5, wave 4: 6-11, 12 = exit global clock
+constexpr int G256_SLOTS = 24;  // wave 0: 0-5, wave 4: 6-11, 12 = exit global clock, 13/14 = stores issued, 15-22 epilogue steps (wave 0)
 __device__ unsigned long long g256_stamp[16384 * G256_SLOTS];
 #define G256_STAMP(slot, val)                                                                        \
   do {                                                                                               \
@@ -740,7 +751,15 @@ __device__ __forceinline__ unsigned xcc_id() {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
   return v & 15;
 }
+#define G256_STEP(slot)                                                                             \
+  do {                                                                                              \
+    if (lane == 0 && wid == 0 && blockIdx.x < 16384)                                                \
+      g256_stamp[blockIdx.x * G256_SLOTS + (slot)] = (unsigned long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
+#define G256_STEP(slot) \
+  do {                  \
+  } while (0)
 #define G256_STAMP(slot, val) \
   do {                        \
   } while (0)
@@ -801,7 +820,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   // row) so the epilogue can run from registers (no LDS stage, no barrier); used when the epilogue
   // is gatherable, else the C^T blocks are staged through LDS transposed
   constexpr bool REG = ALAY == MIT_K_CONTIG && MIT_G256_REGEPI;
-  const bool regepi = REG && ksplit == 1 && epi_gatherable(e);
+  // LDS-staged row-run epilogue for every gatherable epilogue, else the register one
+  constexpr bool LDSEPI = REG && MIT_G256_EPI_LDS && MI == 8;
+  const bool ldsepi = LDSEPI && ksplit == 1 && epi_gatherable(e);
+  const bool regepi = REG && !ldsepi && ksplit == 1 && epi_gatherable(e);
   float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   const int nk = (int)((ke - kb + BK - 1) / BK);
@@ -930,7 +952,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     }
     // register epilogue: the lagging group skips the loop's last barrier (nothing after it reads
     // LDS), so the leading group's epilogue overlaps its last MFMA block and neither waits
-    if (!(regepi && wr == 1 && t + 2 >= nk)) bar_raw();
+    if (!(regepi && wr == 1 && t + 2 >= nk)) bar_raw();  // (never skipped by the LDS-staged epilogue)
   }
 #else
   for (int t = 0; t < nk; t += 2) {
@@ -994,6 +1016,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   struct StampEnd {  // stamps the epilogue's end (stores drained) on every return path
     int lane, wid;
     __device__ ~StampEnd() {
+      if (lane == 0 && (wid == 0 || wid == 4) && blockIdx.x < 16384)  // stores issued, not yet drained
+        g256_stamp[blockIdx.x * G256_SLOTS + 13 + (wid == 4)] = __builtin_amdgcn_s_memtime();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       G256_STAMP(4, __builtin_amdgcn_s_memtime());
       if (wid == 0 && lane == 0 && blockIdx.x < 16384)
@@ -1001,6 +1025,75 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     }
   } stamp_end{lane, wid};
 #endif
+  if constexpr (LDSEPI) {
+    if (ldsepi) {
+      // Two passes over the accumulators: pass p stages row blocks i in [4p, 4p+4) of every wave
+      // (tile rows p*64 .. p*64+63 and 128+p*64 .. +63) as f32 in LDS ([128][256], 16-B chunks
+      // XOR-swizzled by row so the C^T-block writes are conflict-free), then every wave reads back
+      // whole-row runs and runs the same gathered epilogue (epi8x: identical arithmetic, bit-identical
+      // outputs) with its operands loaded in the same coalesced layout before any store.
+      constexpr int EPR = MIT_G256_EPR, LPR = 64 / EPR, CPI = 256 / (LPR * 8);
+      static_assert(EPR == 2 || EPR == 4 || EPR == 8, "MIT_G256_EPR: 2, 4 or 8 rows per store");
+      if (wr == 0) bar_raw();  // re-align the staggered groups: every LDS read of the loop is done
+      bar_raw();
+      G256_STEP(15);
+      auto lrow = [&](int q) { return wid * 16 + (q / CPI) * EPR + lane / LPR; };   // local row 0..127
+      auto lcol = [&](int q) { return (q % CPI) * (LPR * 8) + (lane % LPR) * 8; };  // tile column
+      auto grow = [&](int p, int q) {
+        const int lr = lrow(q);
+        return m0 + (lr >> 6) * 128 + p * 64 + (lr & 63);
+      };
+      auto chunk_off = [](int lr, int ch) { return lr * 1024 + ((ch ^ (lr & 7)) << 4); };
+      auto stage = [&](int p) {  // pass p's accumulators -> LDS (f32, C^T block: lane = row, 4 columns)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int lr = wr * 64 + ii * 16 + (lane & 15);
+            const int ch = wc * 16 + j * 4 + (lane >> 4);
+            *(f32x4*)(smem + chunk_off(lr, ch)) = acc[p * 4 + ii][j];
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar_raw();
+      };
+      auto fetch = [&](int q, float* v) {
+        const int lr = lrow(q), ch = lcol(q) >> 2;
+        const f32x4 a = *(const f32x4*)(smem + chunk_off(lr, ch)), b = *(const f32x4*)(smem + chunk_off(lr, ch + 1));
+        v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+      };
+      float bq[CPI][8];
+#pragma unroll
+      for (int c = 0; c < CPI; ++c) epi_bias8(e, n0 + lcol(c), N, bq[c]);
+      const uint64_t key = epi_key<DROP>(e);
+      bf16x8 x0[8], x1[8];  // residual / aux segments of both passes, loaded before any store
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x0[q] = epi_x8(e, M, N, grow(0, q), n0 + lcol(q));
+      stage(0);
+      G256_STEP(16);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x1[q] = epi_x8(e, M, N, grow(1, q), n0 + lcol(q));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float v[8];
+        fetch(q, v);
+        const long gr = grow(0, q), gc = n0 + lcol(q);
+        if (gr < M && gc < N) epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v, bq[q % CPI], x0[q], key);
+      }
+      G256_STEP(17);
+      bar_raw();  // every wave's pass-0 reads are consumed (used above) before pass 1 overwrites LDS
+      G256_STEP(18);
+      stage(1);
+      G256_STEP(19);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float v[8];
+        fetch(q, v);
+        const long gr = grow(1, q), gc = n0 + lcol(q);
+        if (gr < M && gc < N) epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v, bq[q % CPI], x1[q], key);
+      }
+      return;
+    }
+  }
   if (regepi) {
     // gathered register epilogue: v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane
     // group g with 8 consecutive columns: block 2jp + (g & 1), columns 8 * (g >> 1) .. +8
@@ -1029,7 +1122,45 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
           v[4 + t] = __uint_as_float(sw[1]);
         }
         const long gr = r0 + i * 16, gc = c0 + jp * 32;
+#if MIT_G256_STORE == 3  // diagnostic ONLY (wrong layout, iso shapes): lane-linear, fully coalesced 1-KiB stores
+        {
+          bf16x8 o;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+          *(bf16x8*)((bf16*)C + (((long)blockIdx.x * 8 + wid) * 16 + i * 2 + jp) * 512 + lane * 8) = o;
+        }
+#elif MIT_G256_STORE == 7 || MIT_G256_STORE == 8  // diagnostic ONLY: 1-KiB contiguous runs
+        {
+          const int q = i * 2 + jp;
+#if MIT_G256_STORE == 7  // one 512-column row run per instruction (the next tile's columns too), row per q
+          const long sr = m0 + wid * 16 + q, sc = (n0 / 512) * 512 + lane * 8;
+#else                    // lane-linear 1-KiB pieces, the 8 waves interleaved piece by piece
+          const long lin = ((long)blockIdx.x * 128 + q * 8 + wid) * 512 + lane * 8;
+          const long sr = lin / N, sc = lin % N;
+#endif
+          bf16x8 o;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+          if (sr < M && sc < N) *(bf16x8*)((bf16*)C + sr * ldc + sc) = o;
+        }
+#elif MIT_G256_STORE >= 4  // diagnostic ONLY (wrong values, right coverage): R rows x (512/R) B per store
+        {
+          const int q = i * 2 + jp;
+#if MIT_G256_STORE == 4
+          const long sr = m0 + wid * 32 + q * 2 + (lane >> 5), sc = n0 + (lane & 31) * 8;
+#elif MIT_G256_STORE == 5
+          const long sr = m0 + wid * 32 + (q >> 1) * 4 + (lane >> 4), sc = n0 + (q & 1) * 128 + (lane & 15) * 8;
+#else
+          const long sr = m0 + wid * 32 + (q >> 2) * 8 + (lane >> 3), sc = n0 + (q & 3) * 64 + (lane & 7) * 8;
+#endif
+          bf16x8 o;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+          if (sr < M && sc < N) *(bf16x8*)((bf16*)C + sr * ldc + sc) = o;
+        }
+#else
         if (gr < M && gc < N) epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v, jp ? b1 : b0, xs[i][jp], key);
+#endif
       }
     return;
   }

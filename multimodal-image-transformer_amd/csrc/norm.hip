@@ -390,25 +390,64 @@ void dispatch_nv(long cols, F&& f) {
 // bf16 rows with cols % 8 == 0, cols <= 1024 (every production width: 128 .. 1024): 16-B loads and
 // stores (8 columns per lane per 512-column pass) and RW rows per wave, all their loads issued before
 // the first reduction -- the 8-B-per-lane form moved 38.8 MB per encoder LayerNorm at ~3.5 TB/s
-template <int NV, int RW, bool HASR>
-__global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, const bf16* __restrict__ x, long ldx,
-                                                          const bf16* __restrict__ r, long ldr, const uint64_t* seed,
+// 8 consecutive columns of a row as floats: one 16-B bf16x8 load or two 16-B f32x4 loads
+__device__ __forceinline__ void ld8(const bf16* p, float* v) {
+  const bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = (float)x[k];
+}
+__device__ __forceinline__ void ld8(const float* p, float* v) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = a[k];
+    v[k + 4] = b[k];
+  }
+}
+__device__ __forceinline__ void st8(bf16* p, const float* v) {
+  bf16x8 o;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+  *(bf16x8*)p = o;
+}
+__device__ __forceinline__ void st8(float* p, const float* v) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+// wide rows (cols % 8 == 0, cols <= 1024), 8 columns per lane per 512-column pass, RW rows per wave,
+// every load of the wave's rows issued before the first reduction (so z may alias x: each lane reads
+// its elements before it writes them). TX / TY / TR = input (and z) / output / residual element type:
+// bf16 throughout (the 8-B-per-lane form moved 38.8 MB per encoder LayerNorm at ~3.5 TB/s), or the
+// encoder's f32 residual stream (TX = float) plus a bf16 sublayer output r (TR = bf16), normalised
+// into bf16 or f32 (TY)
+template <int NV, int RW, bool HASR, typename TX = bf16, typename TY = bf16, typename TR = TX>
+__global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, const TX* x, long ldx,
+                                                          const TR* __restrict__ r, long ldr, const uint64_t* seed,
                                                           uint32_t site, uint32_t thresh, float dscale, int dropout,
                                                           const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float eps, bf16* z, bf16* y,
+                                                          const float* __restrict__ beta, float eps, TX* z, TY* y,
                                                           long ldy, float* mean, float* rstd) {
   const int lane = threadIdx.x & 63;
   const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RW;
   const uint64_t key = dropout ? site_key(seed, site) : 0ull;
-  bf16x8 xa[RW][NV], ra[HASR ? RW : 1][NV];
+  float xa[RW][NV][8], ra[HASR ? RW : 1][NV][HASR ? 8 : 1];
 #pragma unroll
   for (int q = 0; q < RW; ++q)
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const long c0 = (long)(i * 64 + lane) * 8, row = row0 + q;
       const bool ok = row < rows && c0 < cols;
-      xa[q][i] = ok ? *(const bf16x8*)(x + row * ldx + c0) : bf16x8{};
-      if (HASR) ra[q][i] = ok ? *(const bf16x8*)(r + row * ldr + c0) : bf16x8{};
+      if (ok) {
+        ld8(x + row * ldx + c0, xa[q][i]);
+        if (HASR) ld8(r + row * ldr + c0, ra[q][i]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xa[q][i][k] = 0.f;
+          if (HASR) ra[q][i][k] = 0.f;
+        }
+      }
     }
 #pragma unroll
   for (int q = 0; q < RW; ++q) {
@@ -420,9 +459,9 @@ __global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, 
       const long c0 = (long)(i * 64 + lane) * 8;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        float a = (float)xa[q][i][k];
+        float a = xa[q][i][k];
         if (HASR) {
-          float b = (float)ra[q][i][k];
+          float b = ra[q][i][k];
           if (dropout) b *= drop_mul(key, (uint64_t)row * (uint64_t)cols + c0 + k, thresh, dscale);
           a += b;
         }
@@ -449,18 +488,14 @@ __global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, 
       if (c0 >= cols) continue;
       const f32x4 g0 = *(const f32x4*)(gamma + c0), g1 = *(const f32x4*)(gamma + c0 + 4);
       const f32x4 b0 = *(const f32x4*)(beta + c0), b1 = *(const f32x4*)(beta + c0 + 4);
-      bf16x8 o, zz;
+      float o[8];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        o[k] = (bf16)((v[i][k] - mu) * rs * g0[k] + b0[k]);
-        o[k + 4] = (bf16)((v[i][k + 4] - mu) * rs * g1[k] + b1[k]);
+        o[k] = (v[i][k] - mu) * rs * g0[k] + b0[k];
+        o[k + 4] = (v[i][k + 4] - mu) * rs * g1[k] + b1[k];
       }
-      if (z) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) zz[k] = (bf16)v[i][k];
-        *(bf16x8*)(z + row * cols + c0) = zz;
-      }
-      *(bf16x8*)(y + row * ldy + c0) = o;
+      if (z) st8(z + row * cols + c0, v[i]);
+      st8(y + row * ldy + c0, o);
     }
     if (lane == 0) {
       if (mean) mean[row] = mu;
@@ -539,6 +574,84 @@ extern "C" int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x,
     else go(float(), std::false_type());
   }
   MIT_LAUNCH_CHECK("mit_layernorm_fwd");
+  return MIT_OK;
+}
+
+// LayerNorm forward of an f32 row stream (the encoder's f32 residual stream): z = x + r (r: the bf16
+// output of the sublayer, may be NULL; z: f32, may be NULL or alias x), y = LN(z) in y_dtype (bf16: the
+// next GEMM's operand; f32: a new residual stream, e.g. CLIP's pre_layrnorm). No saved statistics.
+extern "C" int mit_layernorm_fwd_x32(long rows, long cols, const float* x, long ldx, const void* r, long ldr, float* z,
+                                     const float* gamma, const float* beta, float eps, void* y, int y_dtype, long ldy,
+                                     void* stream) {
+  MIT_RECORD([=]() { return mit_layernorm_fwd_x32(rows, cols, x, ldx, r, ldr, z, gamma, beta, eps, y, y_dtype, ldy, stream); });
+  MIT_CHECK_ARG(x && y && gamma && beta, "mit_layernorm_fwd_x32: null pointer");
+  MIT_CHECK_ARG(y_dtype == MIT_BF16 || y_dtype == MIT_F32, "mit_layernorm_fwd_x32: bad y dtype %d", y_dtype);
+  MIT_CHECK_ARG(cols > 0 && cols % 8 == 0 && cols <= 1024, "mit_layernorm_fwd_x32: cols %ld (multiple of 8, <= 1024)",
+                cols);
+  MIT_CHECK_ARG(ldx >= cols && ldy >= cols && ldx % 8 == 0 && ldy % 8 == 0 && (!r || (ldr >= cols && ldr % 8 == 0)),
+                "mit_layernorm_fwd_x32: bad leading dim");
+  MIT_CHECK_ARG(!z || ldx == cols, "mit_layernorm_fwd_x32: z (row stride cols) needs ldx == cols");
+  MIT_CHECK_ARG((((uintptr_t)x | (uintptr_t)y | (uintptr_t)r | (uintptr_t)z | (uintptr_t)gamma | (uintptr_t)beta) % 16) == 0,
+                "mit_layernorm_fwd_x32: pointers must be 16-B aligned");
+  MIT_CHECK_ARG((const void*)y != (const void*)x && (const void*)y != r, "mit_layernorm_fwd_x32: y must not alias x or r");
+  if (rows <= 0) return MIT_OK;
+  const dim3 g((unsigned)((rows + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  auto go = [&](auto nvc, auto hasr, auto ty) {
+    constexpr int NV = decltype(nvc)::value;
+    constexpr bool HR = decltype(hasr)::value;
+    typedef decltype(ty) TY;
+    hipLaunchKernelGGL((ln_fwd_wide_kernel<NV, 1, HR, float, TY, bf16>), g, dim3(256), 0, s, rows, cols, x, ldx,
+                       (const bf16*)r, ldr, (const uint64_t*)nullptr, 0u, 0u, 0.f, 0, gamma, beta, eps, z, (TY*)y, ldy,
+                       (float*)nullptr, (float*)nullptr);
+  };
+  auto by_r = [&](auto nvc, auto ty) {
+    if (r) go(nvc, std::true_type(), ty);
+    else go(nvc, std::false_type(), ty);
+  };
+  auto by_y = [&](auto nvc) {
+    if (y_dtype == MIT_BF16) by_r(nvc, bf16());
+    else by_r(nvc, float());
+  };
+  if (cols <= 512) by_y(std::integral_constant<int, 1>());
+  else by_y(std::integral_constant<int, 2>());
+  MIT_LAUNCH_CHECK("mit_layernorm_fwd_x32");
+  return MIT_OK;
+}
+
+namespace {
+// y = bf16(x + r): the f32 residual stream's last update, rounded for the consumers (CLIP's
+// last_hidden_state has no final LayerNorm)
+__global__ __launch_bounds__(256) void residual_out_kernel(long rows, long cols, const float* __restrict__ x, long ldx,
+                                                           const bf16* __restrict__ r, long ldr, bf16* __restrict__ y,
+                                                           long ldy) {
+  const long per = cols / 8, n = rows * per;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / per, c = (i - row * per) * 8;
+    float a[8], b[8];
+    ld8(x + row * ldx + c, a);
+    if (r) ld8(r + row * ldr + c, b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += r ? b[k] : 0.f;
+    st8(y + row * ldy + c, a);
+  }
+}
+}  // namespace
+
+extern "C" int mit_residual_out(long rows, long cols, const float* x, long ldx, const void* r, long ldr, void* y, long ldy,
+                                void* stream) {
+  MIT_RECORD([=]() { return mit_residual_out(rows, cols, x, ldx, r, ldr, y, ldy, stream); });
+  MIT_CHECK_ARG(x && y, "mit_residual_out: null pointer");
+  MIT_CHECK_ARG(cols > 0 && cols % 8 == 0 && ldx >= cols && ldy >= cols && ldx % 8 == 0 && ldy % 8 == 0 &&
+                    (!r || (ldr >= cols && ldr % 8 == 0)),
+                "mit_residual_out: cols / leading dims must be multiples of 8");
+  MIT_CHECK_ARG((((uintptr_t)x | (uintptr_t)y | (uintptr_t)r) % 16) == 0, "mit_residual_out: 16-B aligned pointers");
+  if (rows <= 0) return MIT_OK;
+  const long n = rows * (cols / 8);
+  const long blocks = std::min((n + 255) / 256, 8192L);
+  hipLaunchKernelGGL(residual_out_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, rows, cols, x, ldx,
+                     (const bf16*)r, ldr, (bf16*)y, ldy);
+  MIT_LAUNCH_CHECK("mit_residual_out");
   return MIT_OK;
 }
 

@@ -68,6 +68,10 @@ class VisionEncoder:
         self.kin = 3 * self.patch * self.patch
         self.kpad = _round8(self.kin)
         self.device, self.dtype = device, dtype
+        mode = str(getattr(config, "ENCODER_F32_RESIDUAL", "auto")).lower()
+        # f32 residual stream (bf16 compute only): z = h + sublayer(bf16) in f32, fused into the next
+        # LayerNorm (mit_layernorm_fwd_x32), as autocast keeps modeling_vit.py:312-323 / modeling_clip.py:379-393
+        self.res32 = dtype == torch.bfloat16 and (mode in ("on", "1", "true") or (mode == "auto" and self.L >= 24))
         self.w: Dict[str, torch.Tensor] = {}
         self._ws = {}
 
@@ -246,6 +250,12 @@ class VisionEncoder:
                 m=torch.empty(R, self.mlp, dtype=dt, device=dev),
                 out=torch.empty(R, E, dtype=dt, device=dev),
             )
+            if self.res32:  # f32 residual stream, the bf16 sublayer output (delta) and CLIP's f32 embeddings
+                ws = self._ws[key]
+                ws["h32"] = torch.empty(R, E, dtype=torch.float32, device=dev)
+                ws["d"] = torch.empty(R, E, dtype=dt, device=dev)
+                ws["pt32"] = torch.empty(R, E, dtype=torch.float32, device=dev)
+                del ws["pt"], ws["h"]
         return self._ws[key]
 
     def forward(self, images: torch.Tensor, rows: str = "all", slot: int = 0) -> torch.Tensor:
@@ -264,6 +274,10 @@ class VisionEncoder:
         images = images.contiguous().float()
         ws, w, E = self._workspace(B, slot), self.w, self.E
         native.im2col(images, ws["cols"], self.patch, self.kpad)
+        act = native.ACT_GELU if self.kind == "vit" else native.ACT_QUICK_GELU
+        split = max(0, min(self.L, split))
+        if self.res32:
+            return self._forward_res32(B, ws, rows, act, split)
         native.linear(ws["cols"], w["patch.w"], ws["pt"], bias=w["patch.b"])
         h = ws["h"]
         native.vit_assemble(ws["pt"], w["cls"], w["pos"], h, B, self.np, E)
@@ -272,8 +286,6 @@ class VisionEncoder:
             h, ws["a"] = ws["a"], h  # swap roles: the normalised tensor is the residual stream
             ws["h"] = h
         a, qkv, o, m = ws["a"], ws["qkv"], ws["o"], ws["m"]
-        act = native.ACT_GELU if self.kind == "vit" else native.ACT_QUICK_GELU
-        split = max(0, min(self.L, split))
         self._layers(B, h, a, qkv, o, m, act, 0, split)
 
         def rest():
@@ -281,18 +293,71 @@ class VisionEncoder:
             return self._finish(B, ws, h, rows)
         return rest
 
-    def _layers(self, B, h, a, qkv, o, m, act, i0, i1):
+    def _attention(self, B, a, qkv, o, i):
         w, E, N, H = self.w, self.E, self.N, self.H
+        native.linear(a, w[f"{i}.qkv.w"], qkv, bias=w[f"{i}.qkv.b"])
+        args = native.attn_args(qkv, 3 * E, N * 3 * E, qkv[:, E:], 3 * E, N * 3 * E, qkv[:, 2 * E:], 3 * E,
+                                N * 3 * E, o, E, N * E, scale=1.0 / math.sqrt(self.hd))
+        native.attention_fwd(native.dtype_code(qkv), B, H, N, N, args, Dh=self.hd)
+
+    def _layers(self, B, h, a, qkv, o, m, act, i0, i1):
+        w = self.w
         for i in range(i0, i1):
             native.layernorm_fwd(h, w[f"{i}.ln1.w"], w[f"{i}.ln1.b"], self.eps, a)
-            native.linear(a, w[f"{i}.qkv.w"], qkv, bias=w[f"{i}.qkv.b"])
-            args = native.attn_args(qkv, 3 * E, N * 3 * E, qkv[:, E:], 3 * E, N * 3 * E, qkv[:, 2 * E:], 3 * E,
-                                    N * 3 * E, o, E, N * E, scale=1.0 / math.sqrt(self.hd))
-            native.attention_fwd(native.dtype_code(qkv), B, H, N, N, args, Dh=self.hd)
+            self._attention(B, a, qkv, o, i)
             native.linear(o, w[f"{i}.o.w"], h, bias=w[f"{i}.o.b"], residual=h)
             native.layernorm_fwd(h, w[f"{i}.ln2.w"], w[f"{i}.ln2.b"], self.eps, a)
             native.linear(a, w[f"{i}.fc1.w"], m, bias=w[f"{i}.fc1.b"], act=act)
             native.linear(m, w[f"{i}.fc2.w"], h, bias=w[f"{i}.fc2.b"], residual=h)
+
+    def _forward_res32(self, B, ws, rows, act, split):
+        """The same forward with the residual stream h32 in f32: every sublayer output (o-proj, fc2)
+        is written in bf16 to d and added to h32 in f32 by the next LayerNorm (z = h32 + d written back,
+        y = LN(z)), so the stream is never rounded to bf16 -- torch.autocast's arithmetic for the
+        reference's HF layers. Patch embedding, QKV / attention / MLP operands stay bf16."""
+        w, E = self.w, self.E
+        h32, d, a, qkv, o, m = ws["h32"], ws["d"], ws["a"], ws["qkv"], ws["o"], ws["m"]
+        if self.kind == "vit":
+            native.linear(ws["cols"], w["patch.w"], ws["pt32"], bias=w["patch.b"])
+            native.vit_assemble(ws["pt32"], w["cls"], w["pos"], h32, B, self.np, E)
+        else:  # patch + class + positions -> pt32, pre_layrnorm (f32 out) -> the stream h32
+            pt32 = ws["pt32"]
+            native.linear(ws["cols"], w["patch.w"], h32[:B * self.np], bias=w["patch.b"])
+            native.vit_assemble(h32[:B * self.np], w["cls"], w["pos"], pt32, B, self.np, E)
+            native.layernorm_fwd_x32(pt32, w["pre_ln.w"], w["pre_ln.b"], self.eps, h32)
+        state = {"pending": False}
+
+        def layers(i0, i1):
+            for i in range(i0, i1):
+                pend = d if state["pending"] else None
+                native.layernorm_fwd_x32(h32, w[f"{i}.ln1.w"], w[f"{i}.ln1.b"], self.eps, a, r=pend,
+                                         z=h32 if pend is not None else None)
+                self._attention(B, a, qkv, o, i)
+                native.linear(o, w[f"{i}.o.w"], d, bias=w[f"{i}.o.b"])
+                native.layernorm_fwd_x32(h32, w[f"{i}.ln2.w"], w[f"{i}.ln2.b"], self.eps, a, r=d, z=h32)
+                native.linear(a, w[f"{i}.fc1.w"], m, bias=w[f"{i}.fc1.b"], act=act)
+                native.linear(m, w[f"{i}.fc2.w"], d, bias=w[f"{i}.fc2.b"])
+                state["pending"] = True
+
+        layers(0, split)
+
+        def rest():
+            layers(split, self.L)
+            N, out = self.N, ws["out"]
+            pend = d if state["pending"] else None
+            if self.kind == "vit":
+                if rows == "cls":
+                    native.layernorm_fwd_x32(h32, w["final_ln.w"], w["final_ln.b"], self.eps, out, r=pend, rows=B,
+                                             cols=E, ldx=N * E, ldr=N * E, ldy=N * E)
+                    return out.view(B, N, E)[:, 0, :]
+                native.layernorm_fwd_x32(h32, w["final_ln.w"], w["final_ln.b"], self.eps, out, r=pend)
+                return out.view(B, N, E)
+            if rows == "cls":
+                native.residual_out(h32, pend, out, rows=B, cols=E, ldx=N * E, ldr=N * E, ldy=N * E)
+                return out.view(B, N, E)[:, 0, :]
+            native.residual_out(h32, pend, out)
+            return out.view(B, N, E)
+        return rest
 
     def _finish(self, B, ws, h, rows):
         w, E, N = self.w, self.E, self.N

@@ -82,6 +82,8 @@ SIGNATURES = {
     "mit_gemm_grouped_ws_bytes": (L, [ctypes.POINTER(GemmArgs), I]),
     "mit_gemm_grouped": (I, [ctypes.POINTER(GemmArgs), I, ctypes.POINTER(LnGradsJob), I, vp, L, vp]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
+    "mit_layernorm_fwd_x32": (I, [L, L, vp, L, vp, L, vp, vp, vp, Fl, vp, I, L, vp]),
+    "mit_residual_out": (I, [L, L, vp, L, vp, L, vp, L, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
     "mit_layernorm_param_grads": (I, [L, L, vp, vp, vp, vp]),
@@ -506,6 +508,28 @@ def layernorm_fwd(x, gamma, beta, eps, y, *, r=None, drop_p=0.0, seed=None, site
     _check(lib().mit_layernorm_fwd(dtype_code(x), rows, cols, ptr(x), ldx or cols, ptr(r), cols, drop_p, ptr(seed),
                                    site, ptr(gamma), ptr(beta), eps, ptr(z), ptr(y), ldy or cols, ptr(mean),
                                    ptr(rstd), stream_ptr()), "mit_layernorm_fwd")
+
+
+def layernorm_fwd_x32(x, gamma, beta, eps, y, *, r=None, z=None, rows=None, cols=None, ldx=None, ldr=None, ldy=None):
+    """z = x + r (f32; z may be x), y = LN(z) in y's dtype, for the f32 residual stream x
+    (mit_layernorm_fwd_x32; r = the sublayer's bf16 output or None)."""
+    if x.dtype != torch.float32 or (z is not None and z.dtype != torch.float32):
+        raise NativeError("layernorm_fwd_x32: x and z must be f32")
+    if r is not None and r.dtype != torch.bfloat16:
+        raise NativeError("layernorm_fwd_x32: r must be bf16")
+    cols = cols if cols is not None else x.shape[-1]
+    rows = rows if rows is not None else x.numel() // cols
+    _check(lib().mit_layernorm_fwd_x32(rows, cols, ptr(x), ldx or cols, ptr(r), ldr or cols, ptr(z), ptr(gamma), ptr(beta),
+                                       eps, ptr(y), dtype_code(y), ldy or cols, stream_ptr()), "mit_layernorm_fwd_x32")
+
+
+def residual_out(x, r, y, *, rows=None, cols=None, ldx=None, ldr=None, ldy=None):
+    """y (bf16) = x (f32) + r (bf16 or None) (mit_residual_out)."""
+    cols = cols if cols is not None else x.shape[-1]
+    rows = rows if rows is not None else x.numel() // cols
+    _check(lib().mit_residual_out(rows, cols, ptr(x), ldx or cols, ptr(r), ldr or cols, ptr(y), ldy or cols,
+                                  stream_ptr()),
+           "mit_residual_out")
 
 
 def layernorm_bwd_ws_floats(rows, cols):

@@ -222,3 +222,74 @@ def test_incompatible_checkpoint_raises(tmp_path):
     with pytest.raises(TR.CheckpointError):
         TR.load_checkpoint(m, opt, None, str(tmp_path / "b2.pt"))
     assert torch.equal(m.store.master, before)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_weight_edit_through_p_data_is_seen(dtype):
+    """An out-of-band weight edit through p.data (no version-counter bump) reaches the kernels: the
+    autograd forward, evaluation and generation refresh the bf16 shadow every call, and after
+    model.sync_shadow() the fused train step sees it too (params.FlatParams.ensure_shadow)."""
+    meta, _ = FX.load("tiny_vit_patches")
+    m, _ = build_model(meta, dtype)
+    ref, _ = build_model(meta, dtype)
+    m.eval()
+    ref.eval()
+    imgs, di, tg = [t.cuda() for t in FX.inputs(meta, 0)]
+    pm = dict(m.named_parameters())
+    pr = dict(ref.named_parameters())
+    g = torch.Generator().manual_seed(3)
+    new = torch.randn(pm["fc_out.weight"].shape, generator=g).mul_(0.05).cuda()
+    with torch.no_grad():
+        _ = m(imgs, di)  # shadow synced once before the edit
+        pm["fc_out.weight"].data.copy_(new)
+        pr["fc_out.weight"].data.copy_(new)
+        ref.sync_shadow()
+        got, want = m(imgs, di), ref(imgs, di)
+    assert torch.equal(got, want)
+    m.train()
+    ref.train()
+    with torch.no_grad():
+        pm["fc_out.bias"].data.add_(0.25)
+        pr["fc_out.bias"].data.add_(0.25)
+    m.sync_shadow()
+    ref.sync_shadow()
+    assert torch.equal(m.train_step(imgs, di, tg), ref.train_step(imgs, di, tg))
+
+
+def test_torch_adamw_checkpoint_round_trip(tmp_path):
+    """The autograd path's torch.optim.AdamW(model.parameters()) state is saved in the REFERENCE
+    format (train.optimizer_state_reference): the reference-shaped torch.optim.AdamW loads it, and it
+    resumes a fresh model's torch.optim.AdamW -- whose next step then equals the uninterrupted one."""
+    import train as TR
+    meta, _ = FX.load("tiny_vit_patches")
+    kw = dict(lr=meta["lr"], betas=tuple(meta["betas"]), eps=meta["eps"], weight_decay=meta["weight_decay"])
+    crit = nn.CrossEntropyLoss(ignore_index=0)
+    m, st = build_model(meta, torch.float32)
+    m.train()
+    opt = torch.optim.AdamW(m.parameters(), **kw)
+    imgs, di, tg = [t.cuda() for t in FX.inputs(meta, 0)]
+    _reference_step(m, opt, crit, imgs, di, tg, meta["clip_first"])
+    name = TR.save_checkpoint(m, opt, 0, 2.5, str(tmp_path / "tadam"))
+    ck = torch.load(name + ".pt", map_location="cpu", weights_only=True)
+    osd = ck["optimizer_state_dict"]
+    # reference layout: encoder tensors first (no state), then reference_trainable order
+    import optim
+    lay = m.store.layout
+    names = optim.reference_trainable(lay)
+    assert len(osd["param_groups"][0]["params"]) == lay["n_encoder_params"] + len(names)
+    for i, (n, shape) in enumerate(names):
+        assert tuple(osd["state"][lay["n_encoder_params"] + i]["exp_avg"].shape) == shape, n
+    ref_params = [torch.nn.Parameter(torch.zeros(1)) for _ in range(lay["n_encoder_params"])] + \
+        [torch.nn.Parameter(torch.zeros(shape)) for _, shape in names]
+    torch.optim.AdamW(ref_params, **kw).load_state_dict(osd)
+    # resume into a fresh model + torch AdamW, then one more step on both
+    m2, _ = build_model(meta, torch.float32)
+    m2.train()
+    opt2 = torch.optim.AdamW(m2.parameters(), lr=1.0)
+    start, best = TR.load_checkpoint(m2, opt2, None, name + ".pt")
+    assert start == 1 and abs(best - 2.5) < 1e-9 and opt2.param_groups[0]["lr"] == meta["lr"]
+    _, di1, tg1 = [t.cuda() for t in FX.inputs(meta, 1)]
+    l1 = _reference_step(m, opt, crit, imgs, di1, tg1, meta["clip_rest"])
+    l2 = _reference_step(m2, opt2, crit, imgs, di1, tg1, meta["clip_rest"])
+    assert abs(l1 - l2) < 1e-6
+    torch.testing.assert_close(m2.store.master, m.store.master, rtol=1e-5, atol=1e-7)

@@ -391,3 +391,20 @@ def test_generate_batch_row_groups_on_streams_equal_one_group(name, dtype):
     one = m.generate_batch(imgs, 2, 10 ** 6, max_len=14, streams=1)
     for G in (2, 3, 5):
         assert m.generate_batch(imgs, 2, 10 ** 6, max_len=14, streams=G) == one, G
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_generate_batch_plan_graph_eager_agree_with_two_streams(dtype, monkeypatch):
+    """The three launch paths of the per-token step (native launch plan = default, one hipGraph per
+    row group, eager) give the same ids with the batch split into 2 row groups on 2 streams (each
+    group has its own decode state; the groups share the decoder's per-stream defaults)."""
+    m, meta, _ = _trained("tiny_vit_patches", dtype)
+    img = FX.inputs(meta, 0)[0]
+    imgs = torch.cat([img, img.flip(-1), img * 0.5, img.flip(-2)], 0)
+    never = 10 ** 6
+    got = {}
+    for launch in ("plan", "graph", "eager"):
+        monkeypatch.setenv("MIT_DECODE_LAUNCH", launch)
+        got[launch] = m.generate_batch(imgs, 2, never, max_len=20, streams=2)
+    one = m.generate_batch(imgs, 2, never, max_len=20, streams=1)
+    assert got["plan"] == got["graph"] == got["eager"] == one

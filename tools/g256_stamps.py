@@ -21,7 +21,7 @@ import torch  # noqa: E402
 import native  # noqa: E402
 from gemm_bench import SHAPES  # noqa: E402
 
-SLOTS = 16
+SLOTS = 24
 
 
 def stamped(lib, fn, nblk):
@@ -87,8 +87,15 @@ def main(names):
         print(f"  prologue  (us) {q(to_us(mt1 - mt0))}")
         print(f"  K loop    (us) {q(to_us(mt2 - mt1))}  per K-step {np.median(to_us(mt2 - mt1)) / ((K + 63) // 64):.3f}")
         print(f"  epilogue  (us) {q(to_us(mt3 - mt2))}")
+        print(f"  epilogue issue (loop end -> last store issued, us) {q(to_us(s[:, 13] - mt2))}  "
+              f"wave4 {q(to_us(s[:, 14] - w4[:, 2]))}")
         print(f"  wave4 loop-end lag vs wave0 (us) {q(to_us(w4[:, 2] - w4[:, 0] - (mt2 - mt0)))}")
         print(f"  tile total(us) {q(end - start)}")
+        if s[:, 15].any():  # LDS-staged epilogue checkpoints (wave 0)
+            pts = [mt2] + [s[:, k] for k in range(15, 20)] + [s[:, 13]]
+            names = ["realign", "stage0", "pass0 stores issued", "barrier", "stage1", "pass1 stores issued"]
+            print("  epilogue steps (us): " + ", ".join(f"{n} {np.median(to_us(b - a)):.2f}"
+                                                     for n, a, b in zip(names, pts[:-1], pts[1:])))
         order = np.argsort(start)
         rounds = int(np.ceil(nblk / 256))
         for r in range(rounds):
