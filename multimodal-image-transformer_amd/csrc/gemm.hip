@@ -728,7 +728,7 @@ __device__ __forceinline__ void bar_raw() {
 // at ~30 GB/s per CU (4.4-5 us per 256x256 bf16 tile, tools/g256_stamps.py), ~4x slower than
 // long contiguous runs: the store INSTRUCTION pattern, not bytes, bounds the epilogue.
 #ifndef MIT_G256_EPI_LDS
-#define MIT_G256_EPI_LDS 1
+#define MIT_G256_EPI_LDS 0
 #endif
 #ifndef MIT_G256_EPR
 #define MIT_G256_EPR 2
