@@ -57,9 +57,7 @@ struct Epi {
 };
 
 constexpr int ACT_RT = -1;
-#ifndef MIT_G256_STORE  // gathered-epilogue store form (diagnostic builds only, tools/g256_stamps.py)
-#define MIT_G256_STORE 0
-#endif  // activation read from Epi::act at run time (generic instance)
+  // activation read from Epi::act at run time (generic instance)
 
 // FAST: bf16 vector epilogues use the branch-free GELU (gelu_fast, |err| ~1e-7, far below bf16
 // rounding); the scalar / fp32-parity path keeps ocml's erff
@@ -223,13 +221,7 @@ __device__ __forceinline__ void epi8x(const Epi& e, void* C, long ldc, long N, l
     bf16x8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
-#if MIT_G256_STORE == 1  // diagnostic: non-temporal 16-B stores
-    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), (u32x4*)((bf16*)C + r * ldc + c));
-#elif MIT_G256_STORE == 2  // diagnostic ONLY (wrong output): half the bytes, same store count
-    *(u32x2*)((bf16*)C + r * ldc + c) = u32x2{__builtin_bit_cast(u32x4, o)[0], __builtin_bit_cast(u32x4, o)[1]};
-#else
     *(bf16x8*)((bf16*)C + r * ldc + c) = o;
-#endif
   }
 }
 
@@ -1095,73 +1087,56 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     }
   }
   if (regepi) {
-    // gathered register epilogue: v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane
-    // group g with 8 consecutive columns: block 2jp + (g & 1), columns 8 * (g >> 1) .. +8
+    // gathered register epilogue. v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane group g
+    // with 8 consecutive columns of row (lane & 15): block 2jp + (g & 1), columns 8 * (g >> 1) .. +8.
+    // Stored as they are, each instruction would write 16 rows x 64 B (half cache lines): ~3.5x slower
+    // per CU than whole lines (tools/store_bench.hip: 8000 vs 2250 cycles per wave for a tile's 16
+    // stores), the largest fixed cost of a K = 768 tile. So a DPP row_ror:8 exchange swaps the jp = 1
+    // segments of rows 0-7 with the jp = 0 segments of rows 8-15 (lanes l <-> l ^ 8): every store
+    // (and residual / aux load) then covers 8 whole rows x 128 B. Same values, same arithmetic.
     const int g = lane >> 4;
-    const long r0 = m0 + wr * HR + (lane & 15);
-    const long c0 = n0 + wc * 64 + (g & 1) * 16 + (g >> 1) * 8;
-    float b0[8], b1[8];
-    epi_bias8(e, c0, N, b0);
-    epi_bias8(e, c0 + 32, N, b1);
-    bf16x8 xs[MI][2];
+    const bool hi = (lane & 8) != 0;
+    const long rl = m0 + wr * HR + (lane & 7);  // row of store A of row block i: rl + 16 i; store B: + 8
+    const long cl = n0 + wc * 64 + (g & 1) * 16 + (g >> 1) * 8 + (hi ? 32 : 0);
+    float bb[8];
+    epi_bias8(e, cl, N, bb);
+    // residual / aux operands exist only with ACT == NONE on this kernel (mit_gemm routes an activation
+    // plus a residual / aux to the 128 kernel): the activation instances keep no operand registers
+    constexpr bool XOPS = ACT == MIT_ACT_NONE;
+    bf16x8 xs[XOPS ? MI : 1][2];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int jp = 0; jp < 2; ++jp) xs[i][jp] = epi_x8(e, M, N, r0 + i * 16, c0 + jp * 32);
+      for (int h = 0; h < 2; ++h)
+        if constexpr (XOPS) xs[i][h] = epi_x8(e, M, N, rl + i * 16 + h * 8, cl);
     const uint64_t key = epi_key<DROP>(e);
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i) {
+      const bf16x8 x0 = XOPS ? xs[XOPS ? i : 0][0] : bf16x8{}, x1 = XOPS ? xs[XOPS ? i : 0][1] : bf16x8{};
+      float v[2][8];
 #pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        float v[8];
+      for (int jp = 0; jp < 2; ++jp)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][t]),
                                                            __float_as_uint(acc[i][2 * jp + 1][t]), false, false);
-          v[t] = __uint_as_float(sw[0]);
-          v[4 + t] = __uint_as_float(sw[1]);
+          v[jp][t] = __uint_as_float(sw[0]);
+          v[jp][4 + t] = __uint_as_float(sw[1]);
         }
-        const long gr = r0 + i * 16, gc = c0 + jp * 32;
-#if MIT_G256_STORE == 3  // diagnostic ONLY (wrong layout, iso shapes): lane-linear, fully coalesced 1-KiB stores
-        {
-          bf16x8 o;
+      float va[8], vb[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
-          *(bf16x8*)((bf16*)C + (((long)blockIdx.x * 8 + wid) * 16 + i * 2 + jp) * 512 + lane * 8) = o;
-        }
-#elif MIT_G256_STORE == 7 || MIT_G256_STORE == 8  // diagnostic ONLY: 1-KiB contiguous runs
-        {
-          const int q = i * 2 + jp;
-#if MIT_G256_STORE == 7  // one 512-column row run per instruction (the next tile's columns too), row per q
-          const long sr = m0 + wid * 16 + q, sc = (n0 / 512) * 512 + lane * 8;
-#else                    // lane-linear 1-KiB pieces, the 8 waves interleaved piece by piece
-          const long lin = ((long)blockIdx.x * 128 + q * 8 + wid) * 512 + lane * 8;
-          const long sr = lin / N, sc = lin % N;
-#endif
-          bf16x8 o;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
-          if (sr < M && sc < N) *(bf16x8*)((bf16*)C + sr * ldc + sc) = o;
-        }
-#elif MIT_G256_STORE >= 4  // diagnostic ONLY (wrong values, right coverage): R rows x (512/R) B per store
-        {
-          const int q = i * 2 + jp;
-#if MIT_G256_STORE == 4
-          const long sr = m0 + wid * 32 + q * 2 + (lane >> 5), sc = n0 + (lane & 31) * 8;
-#elif MIT_G256_STORE == 5
-          const long sr = m0 + wid * 32 + (q >> 1) * 4 + (lane >> 4), sc = n0 + (q & 1) * 128 + (lane & 15) * 8;
-#else
-          const long sr = m0 + wid * 32 + (q >> 2) * 8 + (lane >> 3), sc = n0 + (q & 3) * 64 + (lane & 7) * 8;
-#endif
-          bf16x8 o;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
-          if (sr < M && sc < N) *(bf16x8*)((bf16*)C + sr * ldc + sc) = o;
-        }
-#else
-        if (gr < M && gc < N) epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v, jp ? b1 : b0, xs[i][jp], key);
-#endif
+      for (int k = 0; k < 8; ++k) {
+        const float snd = hi ? v[0][k] : v[1][k];
+        const float rcv = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd), 0x128, 0xF, 0xF, false));
+        va[k] = hi ? rcv : v[0][k];
+        vb[k] = hi ? v[1][k] : rcv;
       }
+      const long ra = rl + i * 16;
+      if (cl < N) {
+        if (ra < M) epi8x<ACT, DROP>(e, C, ldc, N, ra, cl, va, bb, x0, key);
+        if (ra + 8 < M) epi8x<ACT, DROP>(e, C, ldc, N, ra + 8, cl, vb, bb, x1, key);
+      }
+    }
     return;
   }
   if constexpr (MI == 8) {  // short tiles launch only with the register epilogue (launch_bf16_256)
@@ -1723,7 +1698,8 @@ void launch_layout(const mit_gemm_args* g, const Epi& e, int ab, int bb, const S
       }
     }
   }
-  if (big && k != EK_GENERIC) {
+  // the 256 kernel's activation instances take no residual / aux operand (gemm256_kernel, XOPS)
+  if (big && k != EK_GENERIC && (g->act == MIT_ACT_NONE || (!g->residual && !g->aux))) {
     if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
       switch (k) {
         case EK_RELU: return launch_bf16_256<AL, BL, MIT_ACT_RELU, false>(g, e, ab, bb, s);
@@ -1825,7 +1801,8 @@ extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
   const Split sp = plan_split(g);
   if (ksplit) *ksplit = sp.ks;
   if (sp.ks == 1 && use_rs(g)) return 65;  // the 64x64 register-streaming kernel
-  const bool big = sp.ks == 1 && use_256(g->M, g->N, g->K, g->a_layout) && epi_kind(g) != EK_GENERIC;
+  const bool big = sp.ks == 1 && use_256(g->M, g->N, g->K, g->a_layout) && epi_kind(g) != EK_GENERIC &&
+                   (g->act == MIT_ACT_NONE || (!g->residual && !g->aux));
   return big ? 256 : 128;
 }
 
