@@ -179,6 +179,9 @@ __device__ __forceinline__ bf16x8 epi_x8(const Epi& e, long M, long N, long r, l
   if (src && r < M && c < N) x = *(const bf16x8*)(src + r * (e.res ? e.ldr : e.ld_aux) + c);
   return x;
 }
+// s_waitcnt vmcnt(0) as a builtin (the compiler's waitcnt pass sees it, unlike inline asm): closes a
+// gathered epilogue's load phase (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15)
+__device__ __forceinline__ void gather_wait() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 template <bool DROP>
 __device__ __forceinline__ uint64_t epi_key(const Epi& e) {
   return (DROP && e.dropout) ? site_key(e.seed, e.site) : 0ull;
@@ -309,6 +312,14 @@ __device__ __forceinline__ float frag_rowsum(bf16x8 a, float r) {
   return r;
 }
 
+// workgroup barrier that is also a compiler scheduling / memory fence but emits no vmcnt wait
+// (an in-flight LDS-DMA must survive it)
+__device__ __forceinline__ void bar_raw() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // ------------------------------------------------------------------------------------------------
 // bf16 MFMA kernel, 128x128 block tile
 // ------------------------------------------------------------------------------------------------
@@ -417,9 +428,15 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
       glds_tile<BLAY, 16 / NW>(rb, BS(nb), ldb, N, ke, n0, kb + (long)(kt + PF) * BK, wid, lane);
     }
     wait_tiles<NST, 2 * (16 / NW)>(min(nk - 1 - kt, PF));
-    __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt has landed
+    bar_raw();  // every wave's DMA of tile kt has landed
     compute(cur);
-    __builtin_amdgcn_s_barrier();  // every wave is done reading buffer cur before it is refilled
+    // every wave's fragment reads of buffer cur have RETURNED before any wave refills it: a bare
+    // __builtin_amdgcn_s_barrier() is no memory fence, and hipcc issued the second k-slice's ds_reads
+    // before it with their lgkmcnt waits after, so a fast wave's next DMA could overwrite the buffer
+    // under a slow wave's in-flight reads (seen as run-to-run differences of the decoder GEMMs when
+    // the encoder prefetch shared the chip: tools/diag_race.py)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar_raw();
   }
 #undef AS
 #undef BS
@@ -485,6 +502,7 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
     bf16x8 xs[NP];
 #pragma unroll
     for (int pass = 0; pass < NP; ++pass) xs[pass] = epi_x8(e, M, N, m0 + ((pass * NT + tid) >> 4), gc);
+    gather_wait();
     const uint64_t key = epi_key<DROP>(e);
 #pragma unroll
     for (int pass = 0; pass < NP; ++pass) {
@@ -684,14 +702,6 @@ struct DmaPlan {
   }
 };
 
-// workgroup barrier that is also a compiler scheduling / memory fence but emits no vmcnt wait
-// (an in-flight LDS-DMA must survive it)
-__device__ __forceinline__ void bar_raw() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_barrier" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 // compile-time A/B switches of the 256 kernel (tools/build_variants.sh): row-group height of the
 // tile order and the XCD remap
 #ifndef MIT_G256_GROUP
@@ -756,6 +766,68 @@ __device__ __forceinline__ unsigned xcc_id() {
   do {                        \
   } while (0)
 #endif
+
+// Gathered register epilogue of one wave's (16 MI) x 64 output block, accumulated as C^T blocks
+// (MFMA operands swapped: lane holds row (lane & 15), columns 4 * (lane >> 4) + t of block j); rows
+// from mw, columns from nw. v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane group g
+// with 8 consecutive columns of row (lane & 15): block 2jp + (g & 1), columns 8 * (g >> 1) .. +8.
+// Stored as they are, each instruction would write 16 rows x 64 B (half cache lines): ~3.5x slower
+// per CU than whole lines (tools/store_bench.hip: 8000 vs 2250 cycles per wave for a tile's 16
+// stores), the largest fixed cost of a K = 768 tile. So a DPP row_ror:8 exchange swaps the jp = 1
+// segments of rows 0-7 with the jp = 0 segments of rows 8-15 (lanes l <-> l ^ 8): every store
+// (and residual / aux load) then covers 8 whole rows x 128 B. Same values, same arithmetic.
+template <int ACT, bool DROP, int MI>
+__device__ __forceinline__ void reg_epilogue(const f32x4 (&acc)[MI][4], const Epi& e, void* C, long ldc, long M, long N,
+                                             long mw, long nw, int lane) {
+  const int g = lane >> 4;
+  const bool hi = (lane & 8) != 0;
+  const long rl = mw + (lane & 7);  // row of store A of row block i: rl + 16 i; store B: + 8
+  const long cl = nw + (g & 1) * 16 + (g >> 1) * 8 + (hi ? 32 : 0);
+  float bb[8];
+  epi_bias8(e, cl, N, bb);
+  // residual / aux operands exist only with ACT == NONE on these kernels (mit_gemm routes an
+  // activation plus a residual / aux to the 128 kernel): the activation instances keep no operand registers
+  constexpr bool XOPS = ACT == MIT_ACT_NONE;
+  bf16x8 xs[XOPS ? MI : 1][2];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if constexpr (XOPS) xs[i][h] = epi_x8(e, M, N, rl + i * 16 + h * 8, cl);
+  // every operand load has landed before the first store: the loads sit in exec-masked branches
+  // (bounds, optional operands), after which the compiler cannot count them and waits vmcnt(0) before
+  // each later use -- i.e. behind every store issued so far (vmcnt counts stores): one store round
+  // trip per row block. An explicit wait here clears its scoreboard.
+  gather_wait();
+  const uint64_t key = epi_key<DROP>(e);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const bf16x8 x0 = XOPS ? xs[XOPS ? i : 0][0] : bf16x8{}, x1 = XOPS ? xs[XOPS ? i : 0][1] : bf16x8{};
+    float v[2][8];
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][t]),
+                                                         __float_as_uint(acc[i][2 * jp + 1][t]), false, false);
+        v[jp][t] = __uint_as_float(sw[0]);
+        v[jp][4 + t] = __uint_as_float(sw[1]);
+      }
+    float va[8], vb[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float snd = hi ? v[0][k] : v[1][k];
+      const float rcv = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd), 0x128, 0xF, 0xF, false));
+      va[k] = hi ? rcv : v[0][k];
+      vb[k] = hi ? v[1][k] : rcv;
+    }
+    const long ra = rl + i * 16;
+    if (cl < N) {
+      if (ra < M) epi8x<ACT, DROP>(e, C, ldc, N, ra, cl, va, bb, x0, key);
+      if (ra + 8 < M) epi8x<ACT, DROP>(e, C, ldc, N, ra + 8, cl, vb, bb, x1, key);
+    }
+  }
+}
 
 // MI = 16-row MFMA blocks per wave in M: 8 (256-row tiles) or 5 / 6 (160 / 192-row tiles, K-contig A
 // with the register epilogue only): the N = 768 / 1024 encoder GEMMs (o-proj, fc2) have 150 / 580
@@ -833,8 +905,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     return true;
   };
   auto wait_dma = [&](bool younger_issued) {
+#ifdef MIT_G256_DIAG_NOWAIT  // timing diagnostic only (WRONG results): what the DMA waits cost
+    (void)younger_issued;
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+#else
     if (younger_issued) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   };
 
   bf16x8 af[IH0][2], blo[2][2], bhi[2][2];
@@ -1064,6 +1141,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       G256_STEP(16);
 #pragma unroll
       for (int q = 0; q < 8; ++q) x1[q] = epi_x8(e, M, N, grow(1, q), n0 + lcol(q));
+      gather_wait();
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         float v[8];
@@ -1087,56 +1165,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     }
   }
   if (regepi) {
-    // gathered register epilogue. v_permlane16_swap of column blocks (2jp, 2jp+1) leaves lane group g
-    // with 8 consecutive columns of row (lane & 15): block 2jp + (g & 1), columns 8 * (g >> 1) .. +8.
-    // Stored as they are, each instruction would write 16 rows x 64 B (half cache lines): ~3.5x slower
-    // per CU than whole lines (tools/store_bench.hip: 8000 vs 2250 cycles per wave for a tile's 16
-    // stores), the largest fixed cost of a K = 768 tile. So a DPP row_ror:8 exchange swaps the jp = 1
-    // segments of rows 0-7 with the jp = 0 segments of rows 8-15 (lanes l <-> l ^ 8): every store
-    // (and residual / aux load) then covers 8 whole rows x 128 B. Same values, same arithmetic.
-    const int g = lane >> 4;
-    const bool hi = (lane & 8) != 0;
-    const long rl = m0 + wr * HR + (lane & 7);  // row of store A of row block i: rl + 16 i; store B: + 8
-    const long cl = n0 + wc * 64 + (g & 1) * 16 + (g >> 1) * 8 + (hi ? 32 : 0);
-    float bb[8];
-    epi_bias8(e, cl, N, bb);
-    // residual / aux operands exist only with ACT == NONE on this kernel (mit_gemm routes an activation
-    // plus a residual / aux to the 128 kernel): the activation instances keep no operand registers
-    constexpr bool XOPS = ACT == MIT_ACT_NONE;
-    bf16x8 xs[XOPS ? MI : 1][2];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if constexpr (XOPS) xs[i][h] = epi_x8(e, M, N, rl + i * 16 + h * 8, cl);
-    const uint64_t key = epi_key<DROP>(e);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const bf16x8 x0 = XOPS ? xs[XOPS ? i : 0][0] : bf16x8{}, x1 = XOPS ? xs[XOPS ? i : 0][1] : bf16x8{};
-      float v[2][8];
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][t]),
-                                                           __float_as_uint(acc[i][2 * jp + 1][t]), false, false);
-          v[jp][t] = __uint_as_float(sw[0]);
-          v[jp][4 + t] = __uint_as_float(sw[1]);
-        }
-      float va[8], vb[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float snd = hi ? v[0][k] : v[1][k];
-        const float rcv = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd), 0x128, 0xF, 0xF, false));
-        va[k] = hi ? rcv : v[0][k];
-        vb[k] = hi ? v[1][k] : rcv;
-      }
-      const long ra = rl + i * 16;
-      if (cl < N) {
-        if (ra < M) epi8x<ACT, DROP>(e, C, ldc, N, ra, cl, va, bb, x0, key);
-        if (ra + 8 < M) epi8x<ACT, DROP>(e, C, ldc, N, ra + 8, cl, vb, bb, x1, key);
-      }
-    }
+    reg_epilogue<ACT, DROP, MI>(acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane);
     return;
   }
   if constexpr (MI == 8) {  // short tiles launch only with the register epilogue (launch_bf16_256)
@@ -1182,6 +1211,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       bf16x8 xs[8];
 #pragma unroll
       for (int it = 0; it < 8; ++it) xs[it] = epi_x8(e, M, N, m0 + wr * 128 + pass * 64 + it * 8 + (lane >> 3), gcw);
+      gather_wait();
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int r = it * 8 + (lane >> 3), c8 = (lane & 7) * 8;
@@ -1213,6 +1243,148 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     __builtin_amdgcn_wave_barrier();
   }
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// bf16 MFMA kernel, 256x128 block tile, TWO workgroups per CU (NT: both operands K-contig; the
+// encoder's GEMMs and the decoder's kv_all / fc_out).
+//
+// Why: the 256x256 kernel's epilogue is a per-CU store stream (~11 B per clock per CU: a K = 768
+// tile spends 6-10 us of its 25-29 us writing 128 KiB, tools/g256_stamps.py), and with one
+// workgroup per CU nothing computes meanwhile. Here each CU holds two 4-wave workgroups (72 KiB LDS,
+// <= 256 VGPRs each), so one workgroup's prologue / epilogue runs beside the other's K loop and the
+// ping-pong of the 256 kernel's wave groups comes from the two workgroups instead of a schedule.
+//
+// 4 waves as 2 (M) x 2 (N), 128x64 each (8x4 accumulators, C^T blocks -> register epilogue). K in
+// steps of 32: three LDS stages of 24 KiB (A 256 x 32, B 128 x 32, 64-B rows), filled by LDS-DMA
+// two steps ahead (6 pieces per wave per stage), one barrier per step:
+//   wait vmcnt(6) (this wave's pieces of stage t landed, stage t+1's in flight) -> barrier (every
+//   wave's pieces of t landed; every wave's reads of step t-1 done) -> DMA stage t+2 into the slot of
+//   t-1 -> fragment reads of t -> 32 MFMAs.
+// ------------------------------------------------------------------------------------------------
+constexpr int T2_BK = 32;
+constexpr int T2_A_BYTES = 256 * T2_BK * 2;          // 16 KiB
+constexpr int T2_STAGE = T2_A_BYTES + 128 * T2_BK * 2;  // + B 8 KiB = 24 KiB
+constexpr int T2_NST = 3;
+constexpr int T2_SMEM = T2_NST * T2_STAGE;            // 72 KiB: two workgroups per CU
+#ifndef MIT_GT_GROUP
+#define MIT_GT_GROUP 4
+#endif
+// 16-B chunk c (0..3) of row r in a [rows][32] bf16 image (64-B rows). The chunks of rows 8-15 of
+// every 16-row fragment are XOR 3: the four lane groups of a ds_read_b128 ({0-3,12-15,20-27}, ...)
+// then each cover all 64 banks once (conflict-free fragment reads).
+__device__ __forceinline__ int t2off(int r, int c) { return r * 64 + ((c ^ (((r >> 3) & 1) * 3)) << 4); }
+
+template <int ACT, bool DROP>
+__global__ __launch_bounds__(256, 2) void gemm_tall_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           void* C, long M, long N, long K, long lda, long ldb, long ldc,
+                                                           int a_bytes, int b_bytes, Epi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int nbn = (int)((N + 127) / 128), nbm = (int)((M + 255) / 256);
+  const int ntiles = nbn * nbm;
+  const int bid = xcd_remap(blockIdx.x, ntiles);
+  const int GROUP = MIT_GT_GROUP;  // row groups of GROUP M-tiles walk the N-tiles together (L2 reuse)
+  const int group_id = bid / (GROUP * nbn);
+  const int first_m = group_id * GROUP;
+  const int gsize = min(nbm - first_m, GROUP);
+  const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
+  const int bn = (bid % (GROUP * nbn)) / gsize;
+  const long m0 = (long)bm * 256, n0 = (long)bn * 128;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
+
+  // LDS-DMA plan: piece p (1 KiB = 16 rows x 64 B) of the A image is issued by wave p / 4, of the B
+  // image by wave p / 2; lane l fills row 16p + l / 4, physical chunk l % 4 = logical chunk c ^ swz
+  uint32_t abase[4], bbase[2];
+  int akc[4], bkc[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = (wid * 4 + j) * 16 + (lane >> 2), c = (lane & 3) ^ (((r >> 3) & 1) * 3);
+    akc[j] = c * 8;
+    abase[j] = m0 + r < M ? (uint32_t)(((m0 + r) * lda + c * 8) * 2) : OOB;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = (wid * 2 + j) * 16 + (lane >> 2), c = (lane & 3) ^ (((r >> 3) & 1) * 3);
+    bkc[j] = c * 8;
+    bbase[j] = n0 + r < N ? (uint32_t)(((n0 + r) * ldb + c * 8) * 2) : OOB;
+  }
+  const int nk = (int)((K + T2_BK - 1) / T2_BK);
+  auto issue = [&](int t) {
+    char* st = smem + (t % T2_NST) * T2_STAGE;
+    const uint32_t koff = (uint32_t)t * (T2_BK * 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t boff = (t * T2_BK + akc[j] < K) ? abase[j] + koff : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(st + (wid * 4 + j) * 1024),
+                                               16, boff, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint32_t boff = (t * T2_BK + bkc[j] < K) ? bbase[j] + koff : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (__attribute__((address_space(3))) void*)(st + T2_A_BYTES + (wid * 2 + j) * 1024), 16, boff, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fragment read offsets inside a stage: A row block i of this wave, B column block j
+  const int aoff = t2off(wr * 128 + (lane & 15), lane >> 4);
+  const int boff0 = T2_A_BYTES + t2off(wc * 64 + (lane & 15), lane >> 4);
+
+  // Software pipeline: the fragments of step t+1 are read while step t's MFMAs run (two register
+  // sets, the loop unrolled by two so both are statically named). Step t: wait for this wave's
+  // pieces of stage t+1 and its own reads of stage t -> barrier (stage t+1 visible to all; every
+  // wave's stage-t fragments are in registers, so slot t is free) -> DMA stage t+3 into slot t ->
+  // read stage t+1 -> MFMAs of t. Three slots: t+1 (read now), t+2 (in flight), t+3 (issued now).
+  auto wait_next = [&](int t) {  // this wave's pieces of stage t+1 landed (t+2, if any, may fly)
+    if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  };
+  auto read = [&](int t, bf16x8 (&af)[8], bf16x8 (&bfr)[4]) {
+    const char* st = smem + (t % T2_NST) * T2_STAGE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = __builtin_bit_cast(bf16x8, *(const u32x4*)(st + boff0 + j * 1024));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = __builtin_bit_cast(bf16x8, *(const u32x4*)(st + aoff + i * 1024));
+  };
+  auto mma = [&](const bf16x8 (&af)[8], const bf16x8 (&bfr)[4]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  };
+  auto step = [&](int t, const bf16x8 (&ac)[8], const bf16x8 (&bc)[4], bf16x8 (&an)[8], bf16x8 (&bn)[4]) {
+    if (t + 1 < nk) {
+      wait_next(t);
+      bar_raw();
+      if (t + 3 < nk) issue(t + 3);
+      read(t + 1, an, bn);
+    }
+    mma(ac, bc);
+  };
+
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  if (nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar_raw();
+  bf16x8 a0[8], b0[4], a1[8], b1[4];
+  read(0, a0, b0);
+  for (int t = 0; t < nk; t += 2) {
+    step(t, a0, b0, a1, b1);
+    if (t + 1 < nk) step(t + 1, a1, b1, a0, b0);
+  }
+  reg_epilogue<ACT, DROP, 8>(acc, e, C, ldc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1622,8 +1794,33 @@ int tile_mi(const mit_gemm_args* g, const Epi& e) {
   return best;
 }
 
+template <int ACT, bool DROP>
+void launch_tall(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    set_lds(gemm_tall_kernel<ACT, DROP>, T2_SMEM);
+    attr = true;
+  }
+  const long nb = ((g->M + 255) / 256) * ((g->N + 127) / 128);
+  hipLaunchKernelGGL((gemm_tall_kernel<ACT, DROP>), dim3((unsigned)nb), dim3(256), T2_SMEM, s, (const bf16*)g->A,
+                     (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
+}
+
+// the two-workgroup 256x128 kernel replaces the 256x256 one for NT GEMMs with a register
+// (gathered) epilogue: MIT_GEMM_TALL=0 keeps the 256x256 kernel; variant 7 forces it (tests)
+bool use_tall(const mit_gemm_args* g, const Epi& e) {
+  static int on = -1;
+  if (on < 0) on = getenv("MIT_GEMM_TALL") ? atoi(getenv("MIT_GEMM_TALL")) : 0;
+  if (g->a_layout != MIT_K_CONTIG || g->b_layout != MIT_K_CONTIG || !epi_gatherable(e)) return false;
+  const int v = gemm_variant();
+  return v == 7 || (v == 0 && on);
+}
+
 template <int AL, int BL, int ACT, bool DROP>
 void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
+    if (use_tall(g, e)) return launch_tall<ACT, DROP>(g, e, a_bytes, b_bytes, s);
+  }
   if constexpr (AL == MIT_K_CONTIG) {
     switch (tile_mi(g, e)) {
       case 6: return launch_256_mi<AL, BL, ACT, DROP, 6>(g, e, a_bytes, b_bytes, s);
@@ -1659,7 +1856,7 @@ bool use_rs(const mit_gemm_args* g) {
 bool use_256(long M, long N, long K, int a_layout) {
   const int v = gemm_variant();
   if (v == 1) return false;
-  if (v == 2 || v == 5 || v == 6) return true;
+  if (v == 2 || v == 5 || v == 6 || v == 7) return true;
   // the MN-contig-A instances (weight gradients) exceed 256 VGPRs and spill: 128 kernel (+ split-K)
   if (a_layout != MIT_K_CONTIG) return false;
   if (M < 256 || N < 256 || K < 128) return false;
@@ -1775,7 +1972,7 @@ Split plan_split(const mit_gemm_args* g) {
 }  // namespace
 
 extern "C" int mit_gemm_set_variant(int v) {
-  MIT_CHECK_ARG((v >= 0 && v <= 3) || v == 5 || v == 6, "mit_gemm_set_variant: %d not in {0,1,2,3,5,6}", v);
+  MIT_CHECK_ARG((v >= 0 && v <= 3) || (v >= 5 && v <= 7), "mit_gemm_set_variant: %d not in {0,1,2,3,5,6,7}", v);
   g_variant = v;
   return MIT_OK;
 }

@@ -80,6 +80,7 @@ def test_bench_size_loss_decreases():
     def step():
         m.train_step(images, di, tg, next_images=images)
         opt.step(5.0)
+    opt._sync_lr()  # the lr lives in device memory: set it outside the recorded launches
     progs = [native.record(step) for _ in range(2)]
     losses = []
     for k in range(5):
@@ -89,3 +90,23 @@ def test_bench_size_loss_decreases():
     assert all(math.isfinite(x) for x in losses), losses
     assert all(x < losses[0] for x in losses[1:]), losses
     assert losses[-1] < min(losses[:-1]), losses
+
+
+def test_bench_size_prefetch_is_bitwise_neutral():
+    """The encoder prefetch stream shares the chip with the step's decoder kernels: 3 steps with and
+    without it must give bit-identical losses and master weights (a latent LDS WAR race in the 128-tile
+    GEMM only showed under that concurrency, tools/diag_race.py)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = []
+    for prefetch in (False, True, True):
+        m, opt, images, di, tg = _model(1e-4)
+        losses = []
+        for _ in range(3):
+            losses.append(m.train_step(images, di, tg, next_images=images if prefetch else None).item())
+            opt.step(5.0)
+        res.append((losses, m.store.master.clone()))
+        del m, opt
+    for losses, master in res[1:]:
+        assert losses == res[0][0], (losses, res[0][0])
+        assert torch.equal(master, res[0][1])

@@ -229,3 +229,47 @@ def test_gemm256_short_tiles_bit_identical(M, Nn, K, epi):
         assert _rel(outs[2], ref) < 8e-3
     for v in (6, 5):
         assert torch.equal(outs[v], outs[2]), f"variant {v}"
+
+
+TALL_SHAPES = [(256, 128, 32), (264, 136, 72), (520, 776, 200), (1000, 520, 136), (2056, 768, 1536), (12608, 2304, 768)]
+
+
+@pytest.mark.parametrize("M,Nn,K", TALL_SHAPES)
+def test_gemm_tall_bit_identical_to_256(M, Nn, K):
+    """The two-workgroup 256x128 kernel (gemm_tall_kernel, variant 7) runs every output element's MFMAs
+    in the same K order as the 256x256 kernel (32-deep chunks in sequence), so NT outputs are
+    bit-identical; and within the fp32 reference's tolerance."""
+    A, B, ref = _ops(M, Nn, K, 0, 0, seed=4)
+    g = torch.Generator().manual_seed(6)
+    bias = torch.randn(Nn, generator=g).to(dev())
+    res = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
+    seed = torch.tensor([5], dtype=torch.int64, device=dev())
+    cases = [dict(f32=True), dict(bias=bias), dict(bias=bias, act=N.ACT_GELU), dict(residual=res),
+             dict(bias=bias, act=N.ACT_RELU, drop_p=0.1, seed=seed, site=3), dict(bias=bias, act=N.ACT_QUICK_GELU)]
+    for kw in cases:
+        f32 = kw.pop("f32", False)
+        outs = []
+        for v in (7, 2):
+            N.gemm_set_variant(v)
+            C = torch.empty(M, Nn, device=dev(), dtype=torch.float32 if f32 else torch.bfloat16)
+            N.gemm(A, B, C, M, Nn, K, **kw)
+            outs.append(C)
+        assert torch.equal(outs[0], outs[1]), (kw.keys(), (outs[0].float() - outs[1].float()).abs().max().item())
+        if f32:
+            assert _rel(outs[0], ref) < 1e-5
+
+
+def test_gemm_tall_race_screen():
+    N.gemm_set_variant(7)
+    M, Nn, K = 4104, 2312, 776
+    A, B, ref = _ops(M, Nn, K, 0, 0, seed=7)
+    C0 = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
+    N.gemm(A, B, C0, M, Nn, K)
+    assert _rel(C0, ref) < 8e-3
+    C = torch.empty_like(C0)
+    bad = 0
+    for _ in range(30):
+        C.fill_(0)
+        N.gemm(A, B, C, M, Nn, K)
+        bad += int(not torch.equal(C, C0))
+    assert bad == 0, f"{bad}/30 repeats differ bitwise (LDS race)"
