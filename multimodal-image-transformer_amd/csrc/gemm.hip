@@ -735,6 +735,12 @@ struct DmaPlan {
 #ifndef MIT_G256_EPR
 #define MIT_G256_EPR 2
 #endif
+// bf16 outputs through each wave's private LDS stage (stage_epilogue) instead of the register
+// exchange (reg_epilogue)
+#ifndef MIT_G256_EPI_STAGE
+#define MIT_G256_EPI_STAGE 1
+#endif
+
 
 // Diagnostic build only (-DMIT_G256_STAMP, tools/g256_stamps.py): per workgroup, wave 0 and wave 4 stamp
 // the shader clock (s_memtime) at entry, after the prologue's first barrier, after the K loop and after
@@ -829,11 +835,124 @@ __device__ __forceinline__ void reg_epilogue(const f32x4 (&acc)[MI][4], const Ep
   }
 }
 
+// LDS-staged bf16 epilogue of one wave's 128 x 64 block (C^T accumulators as above), through the
+// wave's PRIVATE 16 KiB of LDS (no barrier): the fused epilogue (alpha, bias, activation, aux mask,
+// dropout, residual) runs in f32 in the accumulator layout -- lane = row 16 i + (lane & 15), columns
+// 16 j + 4 g + t, g = lane >> 4 -- rounds once to bf16, writes 4 bf16 per (i, j) with ds_write_b64, and
+// reads whole 8-column chunks back for stores of 8 rows x 128 B. A residual / aux block is loaded in
+// that same whole-line pattern before any store, written to the image, and read back per (i, j) segment
+// just before the output segment overwrites it (the LDS does the transpose). Replaces reg_epilogue's
+// permlane16_swap / DPP exchange and its selects (~40 VALU per 16-row block per wave): the epilogue of
+// a K = 768 tile is VALU-bound. Measured (tools/g256_stamps.py, 8 tiles): plain 4.1 -> 2.4 us, residual
+// 5.9 -> 4.8 us; enc qkv+bias 51.1 -> 48.8 us, fc1 73.8 -> 68.8, kv_all 102 -> 94.7; residual loads as
+// 8-B segments in the accumulator layout instead: slower (o+res 28.6 -> 31.9 us). Image: row r at
+// r * 128 B, 16-B chunk c at (c ^ (r & 7)) * 16 (the 8-row x 8-chunk read-back is conflict-free).
+template <int ACT, bool DROP, bool XOPS>
+__device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const Epi& e, void* C, long ldc, long M,
+                                               long N, long mw, long nw, int lane, char* stg) {
+  const int g = lane >> 4, r16 = lane & 15;
+  float bj[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long c = nw + 16 * j + 4 * g;
+    if (e.bias && c < N) {
+      const f32x4 b = *(const f32x4*)(e.bias + c);
+      bj[j][0] = b[0]; bj[j][1] = b[1]; bj[j][2] = b[2]; bj[j][3] = b[3];
+    } else {
+      bj[j][0] = bj[j][1] = bj[j][2] = bj[j][3] = 0.f;
+    }
+  }
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  const long cw = nw + 8 * (lane & 7);
+  if constexpr (XOPS) {
+    // the residual / aux block arrives in whole-line loads (8 rows x 128 B per instruction, the store
+    // pattern) and is transposed to the accumulator layout through the same LDS image: each (i, j)
+    // segment is read back (ds_read_b64) right before the output segment overwrites it
+    const bf16* src = (const bf16*)(e.res ? e.res : e.aux);
+    const long ldx = e.res ? e.ldr : e.ld_aux;
+    u32x4 xl[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const long row = mw + 8 * q + (lane >> 3);
+      xl[q] = (row < M && cw < N) ? *(const u32x4*)(src + row * ldx + cw) : u32x4{0u, 0u, 0u, 0u};
+    }
+    gather_wait();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rr = 8 * q + (lane >> 3);
+      *(u32x4*)(stg + rr * 128 + (((lane & 7) ^ (rr & 7)) << 4)) = xl[q];
+    }
+  } else {
+    gather_wait();
+  }
+  const uint64_t key = epi_key<DROP>(e);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rr = 16 * i + r16;
+    const long row = mw + rr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t] * e.alpha + bj[j][t];
+      if (ACT == MIT_ACT_GELU) {
+#pragma unroll
+        for (int t = 0; t < 4; t += 2) {
+          const f32x2 q = gelu_fast2(f32x2{v[t], v[t + 1]});
+          v[t] = q[0];
+          v[t + 1] = q[1];
+        }
+      } else if (ACT != MIT_ACT_NONE) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = act_apply<ACT, true>(e.act, v[t]);
+      }
+      const int ch = 2 * j + (g >> 1);
+      char* seg = stg + rr * 128 + ((ch ^ (rr & 7)) << 4) + (g & 1) * 8;
+      if constexpr (XOPS) {
+        const u32x2 x = *(const u32x2*)seg;
+        const float x0 = __uint_as_float(x[0] << 16), x1 = __uint_as_float(x[0] & 0xFFFF0000u);
+        const float x2 = __uint_as_float(x[1] << 16), x3 = __uint_as_float(x[1] & 0xFFFF0000u);
+        if (e.aux) {
+          v[0] *= x0 > 0.f ? e.aux_scale : 0.f;
+          v[1] *= x1 > 0.f ? e.aux_scale : 0.f;
+          v[2] *= x2 > 0.f ? e.aux_scale : 0.f;
+          v[3] *= x3 > 0.f ? e.aux_scale : 0.f;
+        }
+        if (DROP && e.dropout) {
+          const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)(nw + 16 * j + 4 * g);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] *= drop_mul(key, base + t, e.thresh, e.dscale);
+        }
+        if (e.res) {
+          v[0] += x0;
+          v[1] += x1;
+          v[2] += x2;
+          v[3] += x3;
+        }
+      } else if (DROP && e.dropout) {
+        const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)(nw + 16 * j + 4 * g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] *= drop_mul(key, base + t, e.thresh, e.dscale);
+      }
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *(bf16x4*)seg = o;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int rr = 8 * q + (lane >> 3);
+    const u32x4 o = *(const u32x4*)(stg + rr * 128 + (((lane & 7) ^ (rr & 7)) << 4));
+    const long row = mw + rr;
+    if (row < M && cw < N) *(u32x4*)((bf16*)C + row * ldc + cw) = o;
+  }
+}
+
 // MI = 16-row MFMA blocks per wave in M: 8 (256-row tiles) or 5 / 6 (160 / 192-row tiles, K-contig A
 // with the register epilogue only): the N = 768 / 1024 encoder GEMMs (o-proj, fc2) have 150 / 580
 // 256-row tiles -- one round on 150 of 256 CUs, or a third round for 68 tiles -- and shorter tiles fill
 // the rounds (mit_gemm picks per shape, tile_rounds_cost)
-template <int ALAY, int BLAY, int ACT, bool DROP, int MI = 8>
+template <int ALAY, int BLAY, int ACT, bool DROP, int MI = 8, int STG = 0>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                       long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
                                                       int b_bytes, Epi e, int ksplit, long kchunk,
@@ -888,6 +1007,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   constexpr bool LDSEPI = REG && MIT_G256_EPI_LDS && MI == 8;
   const bool ldsepi = LDSEPI && ksplit == 1 && epi_gatherable(e);
   const bool regepi = REG && !ldsepi && ksplit == 1 && epi_gatherable(e);
+  // LDS-staged bf16 epilogue (stage_epilogue) for bf16 outputs of the 256-row tile
+  // STG (launch_256_mi, bf16 out): the LDS-staged epilogue, 1 = no operand, 2 = with the residual /
+  // aux operand. A template flag, not a run-time branch: two epilogues in one instance spill in the K loop
+  const bool stage = STG && MI == 8 && regepi;
   float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   const int nk = (int)((ke - kb + BK - 1) / BK);
@@ -1014,6 +1137,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     issue(0, 1, t + 2);
 #endif
     wait_dma(issue(1, 0, t + 3));
+    // staged epilogue: the lagging group writes its LDS stage into the last K-tile's buffer right after
+    // its last MFMA block, so every wave's reads of that buffer must have RETURNED by this (for group 1:
+    // its last) barrier, not only been issued
+    if (stage && t + 2 >= nk) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar_raw();
     if (two) {
       mma(1, 1, bhi);
@@ -1165,6 +1292,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     }
   }
   if (regepi) {
+    if constexpr (MI == 8 && STG) {
+      if (stage) {
+        // group 0 stages into the buffer NOT holding the last K-tile (its last reads were >= 2 phases
+        // ago), group 1 into the last K-tile's buffer (every read of it returned by the last barrier)
+        const int buf = wr == 0 ? (nk & 1) : ((nk - 1) & 1);
+        char* stg = smem + buf * BUF_BYTES + wc * 16384;
+        stage_epilogue<ACT, DROP, STG == 2>(acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane, stg);
+        return;
+      }
+    }
     reg_epilogue<ACT, DROP, MI>(acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane);
     return;
   }
@@ -1745,7 +1882,33 @@ void launch_256_mi(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_byte
   static bool attr = false;
   if (!attr) {
     set_lds(gemm256_kernel<AL, BL, ACT, DROP, MI>, SMEM2_BYTES);
+    if constexpr (MI == 8 && AL == MIT_K_CONTIG) {
+      set_lds(gemm256_kernel<AL, BL, ACT, DROP, MI, 1>, SMEM2_BYTES);
+      if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, MI, 2>, SMEM2_BYTES);
+    }
     attr = true;
+  }
+  if constexpr (MI == 8 && AL == MIT_K_CONTIG && MIT_G256_EPI_STAGE) {
+    // MIT_G256_STAGE: 0 = register epilogue everywhere, 1 = staged without operands only, 2 = staged
+    // everywhere it applies (default)
+    static const int on = getenv("MIT_G256_STAGE") ? atoi(getenv("MIT_G256_STAGE")) : 2;
+    const bool ops = e.res || e.aux;
+    if (on && epi_gatherable(e) && !e.out_f32 && (!ops || on == 2)) {
+      if constexpr (ACT == MIT_ACT_NONE) {
+        if (ops) {
+          hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, MI, 2>), dim3((unsigned)(nbm * nbn)), dim3(512),
+                             SMEM2_BYTES, s, (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda,
+                             g->ldb, g->ldc, a_bytes, b_bytes, e, 1, g->K, (float*)g->workspace, g->rowsum);
+          return;
+        }
+      }
+      if (!ops) {
+        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, MI, 1>), dim3((unsigned)(nbm * nbn)), dim3(512),
+                           SMEM2_BYTES, s, (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb,
+                           g->ldc, a_bytes, b_bytes, e, 1, g->K, (float*)g->workspace, g->rowsum);
+        return;
+      }
+    }
   }
   hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, MI>), dim3((unsigned)(nbm * nbn)), dim3(512), SMEM2_BYTES, s,
                      (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
