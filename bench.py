@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
-PMC_SUMMARY = "r02_pmc.json"
+PMC_SUMMARY = "r03_pmc.json"
 METRIC = "image-caption pairs/sec (train step), 6L/d512 decoder + ViT-B/16, 1/2/4/8 GPU"
 
 
@@ -169,7 +169,7 @@ class GemmProbe:
 def pmc_traffic(kernel_prefix):
     """HBM bytes per launch of a kernel (averaged over the launches of all its template instances)
     from the committed rocprofv3 PMC summary (FETCH_SIZE and
-    WRITE_SIZE passes of tools/profile_r02.sh over this same command, condensed by
+    WRITE_SIZE passes of tools/profile_round.sh over this same command, condensed by
     tools/rocpd_summary.py); None when no summary is present."""
     path = os.path.join(ROOT, "profiles", PMC_SUMMARY)
     try:

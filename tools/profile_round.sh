@@ -8,9 +8,10 @@
 # Condense with tools/rocpd_summary.py into profiles/.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/prof_r02
+TAG=${1:-r03}
+OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-ARGS="--no-cpu-baseline --steps 10 --warmup 3"
+ARGS="--no-cpu-baseline --no-also --steps 10 --warmup 3"
 P="rocprofv3 --output-format rocpd csv"
 timeout -k 10 300 $P --kernel-trace --stats -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.json 2> $OUT/trace.err &&
 timeout -k 10 300 $P --kernel-trace --stats -d $OUT/trace_noprefetch -o run -- python3 bench.py $ARGS --no-prefetch --no-roofline > $OUT/trace_noprefetch.json 2> $OUT/trace_noprefetch.err &&

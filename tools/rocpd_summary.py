@@ -1,4 +1,4 @@
-"""Condense rocprofv3 rocpd databases (tools/profile_r02.sh) into the summaries committed under
+"""Condense rocprofv3 rocpd databases (tools/profile_round.sh) into the summaries committed under
 profiles/ (the --stats tables themselves, run_kernel_stats.csv, are copied there as they are):
 
   <prefix>_pmc.json          per-kernel FETCH_SIZE / WRITE_SIZE averages (separate passes) and the
