@@ -470,6 +470,29 @@ constexpr int HK_MAX = 640;  // keys per head the LDS can hold (K + V = 256 B pe
 #endif
 constexpr float LAZY_LOG2 = MIT_ATTN_LAZY;
 
+// cross-lane reductions over the 4 lane groups of a 16-query tile (lanes l, l ^ 16, l ^ 32, l ^ 48
+// hold one query's key groups): v_permlane16_swap / v_permlane32_swap of a value with itself leave
+// the (l, l ^ 16) / (l, l ^ 32) pair in the two results -- VALU, no LDS round trip
+__device__ __forceinline__ float xmax_rows(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __builtin_fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __builtin_fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float xsum_rows(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float max16(const float (&s)[16]) {
+  const float a = __builtin_fmaxf(__builtin_fmaxf(s[0], s[1]), s[2]), b = __builtin_fmaxf(__builtin_fmaxf(s[3], s[4]), s[5]);
+  const float c = __builtin_fmaxf(__builtin_fmaxf(s[6], s[7]), s[8]), d = __builtin_fmaxf(__builtin_fmaxf(s[9], s[10]), s[11]);
+  const float e = __builtin_fmaxf(__builtin_fmaxf(s[12], s[13]), s[14]);
+  return __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(a, b), c), __builtin_fmaxf(__builtin_fmaxf(d, e), s[15]));
+}
+constexpr bf16x8 ones8 = {(bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f};
+
 template <bool DROP>
 __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) void attn_fwd_head(long H, long Lq, long Lk, AttnK a, int kbytes, int vbytes,
                                                       int lkp) {
@@ -528,6 +551,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
 #pragma unroll
     for (int i = 0; i < 4; ++i) ot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, l = 0.f;
+    f32x4 lacc = {0.f, 0.f, 0.f, 0.f};  // MFMA-accumulated denominator of the full chunks (!DROP)
     const char* Kc = Ks;
     const char* Vc = Vs;
     int j0 = 0;
@@ -563,11 +587,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
         for (int k = 0; k < 16; ++k)
           if (j0 + (k >> 2) * 16 + g * 4 + (k & 3) >= Lk) s[k] = -INFINITY;
       }
-      float tmax = s[0];
-#pragma unroll
-      for (int k = 1; k < 16; ++k) tmax = __builtin_fmaxf(tmax, s[k]);
-      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      // row max: v_max3 tree over the 16 in-lane scores, then the query's 4 lane groups (l, l ^ 16,
+      // l ^ 32, l ^ 48) through v_permlane16/32_swap (VALU) instead of ds_bpermute round trips
+      float tmax = max16(s);
+      tmax = xmax_rows(tmax);
       // lazy rescale (the kernel is VALU-bound): the running max m moves only when some row's chunk
       // max exceeds it by more than LAZY_LOG2 (wave-uniform); otherwise p = 2^(s - m) <= 2^LAZY_LOG2,
       // in range for bf16 P and the f32 sums, and l / O need no rescale. O = ot / l is unchanged.
@@ -576,19 +599,20 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
         const float mnew = __builtin_fmaxf(m, cand);
         const float alpha = __builtin_amdgcn_exp2f(m - mnew);
         l *= alpha;
+        lacc *= alpha;
 #pragma unroll
         for (int i = 0; i < 4; ++i) ot[i] *= alpha;
         m = mnew;
       }
-      float p[16], psum = 0.f;
+      float p[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        p[k] = __builtin_amdgcn_exp2f(fmaf(s[k], sl2, -m));
-        psum += p[k];
+      for (int k = 0; k < 16; ++k) p[k] = __builtin_amdgcn_exp2f(fmaf(s[k], sl2, -m));
+      if (DROP) {  // the denominator sums the undropped p (VALU); without dropout an MFMA sums them below
+        float psum = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) psum += p[k];
+        l += xsum_rows(psum);
       }
-      psum += __shfl_xor(psum, 16, 64);
-      psum += __shfl_xor(psum, 32, 64);
-      l += psum;
       if (DROP) {
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb)
@@ -605,8 +629,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           ot[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv[hh][i]), pb, ot[i], 0, 0, 0);
+        // softmax denominator: ones^T P^T = the query's sum of its 32 (bf16) p in every accumulator
+        // row -- one MFMA instead of 16 VALU adds and two cross-lane reductions
+        if (!DROP) lacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb, lacc, 0, 0, 0);
       }
     }
+    if (!DROP) l += lacc[0];
     // ---- tail: the last 16 / 32 / 48 keys (K/V are staged to a multiple of 16 rows, not 64) ----
     const int ntail = (lkp - j0) >> 4;  // wave-uniform
     if (ntail) {
@@ -628,8 +656,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
       float tmax = s[0];
 #pragma unroll
       for (int k = 1; k < 12; ++k) tmax = __builtin_fmaxf(tmax, s[k]);
-      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = __builtin_fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = xmax_rows(tmax);
       const float mnew = __builtin_fmaxf(m, tmax * sl2);  // finite: key j0 < Lk
       const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       float p[12], psum = 0.f;
@@ -638,9 +665,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
         p[k] = __builtin_amdgcn_exp2f(fmaf(s[k], sl2, -mnew));
         psum += p[k];
       }
-      psum += __shfl_xor(psum, 16, 64);
-      psum += __shfl_xor(psum, 32, 64);
-      l = l * alpha + psum;
+      l = l * alpha + xsum_rows(psum);
       m = mnew;
       if (DROP) {
 #pragma unroll

@@ -119,38 +119,79 @@ __global__ void embed_bwd_kernel(long B, long T_, long d, const int64_t* __restr
 
 // Deterministic embedding backward (replaces the float atomics above): the gradient row of token v
 // is the sum over the positions holding v, taken in a FIXED order. Plan (depends on the tokens
-// only): ONE workgroup bitonic-sorts the (token << 20 | position) keys in LDS (n <= 16384, so the
-// step's 4032 positions sort in 78 compare-exchange stages of one block), then plan[k] = position
-// of sorted slot k and plan[n + k] = the length of the token's run starting at k (0 if slot k is not
-// the first of its token).
+// only): ONE 1024-thread workgroup bitonic-sorts the (token << 20 | position) keys, then
+// plan[k] = position of sorted slot k and plan[n + k] = the length of the token's run starting at k
+// (0 if slot k is not the first of its token). Each thread keeps KPT consecutive keys in registers:
+// compare-exchange distances j < KPT stay in the thread, KPT <= j < 64 KPT cross lanes of one wave
+// (__shfl_xor), and only j >= 64 KPT go through LDS (2 barriers each) -- 10 of the 78 stages at
+// n = 4032 (was: all 78 through LDS behind a barrier each, 86 us per step).
 constexpr int EMB_PLAN_MAX = 16384;
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v, m, 64);
+  const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+template <int KPT>
 __global__ __launch_bounds__(1024) void embed_plan_kernel(const int64_t* __restrict__ tok, int n, int npow2,
                                                           int* __restrict__ plan) {
   extern __shared__ uint64_t keys[];
-  for (int i = threadIdx.x; i < npow2; i += 1024)
-    keys[i] = i < n ? ((uint64_t)tok[i] << 20) | (uint64_t)i : ~0ull;
-  __syncthreads();
-  for (int k = 2; k <= npow2; k <<= 1)
+  const int t = threadIdx.x;
+  uint64_t x[KPT];
+#pragma unroll
+  for (int e = 0; e < KPT; ++e) {
+    const int i = t * KPT + e;
+    x[e] = i < n ? ((uint64_t)tok[i] << 20) | (uint64_t)i : ~0ull;
+  }
+  for (int k = 2; k <= npow2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < npow2; i += 1024) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t x = keys[i], y = keys[ixj];
-          if ((x > y) == ((i & k) == 0)) {
-            keys[i] = y;
-            keys[ixj] = x;
+      if (j < KPT) {  // both elements in this thread
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) {
+          const int f = e ^ j;
+          if (f > e) {
+            const bool asc = ((t * KPT + e) & k) == 0;
+            const uint64_t a = x[e], b = x[f];
+            if ((a > b) == asc) {
+              x[e] = b;
+              x[f] = a;
+            }
           }
         }
+      } else if (j < 64 * KPT) {  // partner element = same slot of lane ^ (j / KPT)
+        const int m = j / KPT;
+        const bool lower = (t & m) == 0;
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) {
+          const uint64_t o = shfl_xor_u64(x[e], m);
+          const bool asc = ((t * KPT + e) & k) == 0;
+          x[e] = (lower == asc) ? (x[e] < o ? x[e] : o) : (x[e] > o ? x[e] : o);
+        }
+      } else {
+        const int m = j / KPT;
+        const bool lower = (t & m) == 0;
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) keys[t * KPT + e] = x[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < KPT; ++e) {
+          const uint64_t o = keys[(t ^ m) * KPT + e];
+          const bool asc = ((t * KPT + e) & k) == 0;
+          x[e] = (lower == asc) ? (x[e] < o ? x[e] : o) : (x[e] > o ? x[e] : o);
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
-  for (int k = threadIdx.x; k < n; k += 1024) {
-    const uint64_t t = keys[k] >> 20;
+  }
+#pragma unroll
+  for (int e = 0; e < KPT; ++e) keys[t * KPT + e] = x[e];
+  __syncthreads();
+  for (int k = t; k < n; k += 1024) {
+    const uint64_t tk = keys[k] >> 20;
     plan[k] = (int)(keys[k] & 0xFFFFFu);
     int len = 0;
-    if (k == 0 || (keys[k - 1] >> 20) != t) {
+    if (k == 0 || (keys[k - 1] >> 20) != tk) {
       len = 1;
-      while (k + len < n && (keys[k + len] >> 20) == t) ++len;
+      while (k + len < n && (keys[k + len] >> 20) == tk) ++len;
     }
     plan[n + k] = len;
   }
@@ -175,9 +216,9 @@ __global__ __launch_bounds__(256) void embed_bwd_seg_kernel(int n, int d, const 
   const int lane = threadIdx.x & 63;
   const uint64_t key = dropout ? site_key(seed, site) : 0ull;
   // a token's rows are summed in position order, ER rows' loads in flight at a time (the run of a
-  // token every caption has -- START at position 0 -- is B rows long: one dependent load per row
-  // made it the longest wave of the kernel)
-  constexpr int ER = 8;
+  // token every caption has -- START at position 0 -- is B rows long and sits on the backward's
+  // critical path: one dependent load per row made it the longest wave of the kernel)
+  constexpr int ER = 16;
   for (int c0 = lane * 8; c0 < d; c0 += 512) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int r0 = 0; r0 < len; r0 += ER) {
@@ -538,13 +579,23 @@ extern "C" int mit_embed_plan(const int64_t* tokens, long n, int* plan, void* st
   if (n == 0) return MIT_OK;
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
+  if (np2 < 1024) np2 = 1024;  // one key slot per thread at least (pads sort last)
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)embed_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)embed_plan_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              EMB_PLAN_MAX * 8);
+    (void)hipFuncSetAttribute((const void*)embed_plan_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               EMB_PLAN_MAX * 8);
     attr = true;
   }
-  hipLaunchKernelGGL(embed_plan_kernel, dim3(1), dim3(1024), np2 * 8, (hipStream_t)stream, tokens, (int)n, np2, plan);
+  hipStream_t s = (hipStream_t)stream;
+  switch (np2 / 1024) {
+    case 1: hipLaunchKernelGGL(embed_plan_kernel<1>, dim3(1), dim3(1024), np2 * 8, s, tokens, (int)n, np2, plan); break;
+    case 2: hipLaunchKernelGGL(embed_plan_kernel<2>, dim3(1), dim3(1024), np2 * 8, s, tokens, (int)n, np2, plan); break;
+    case 4: hipLaunchKernelGGL(embed_plan_kernel<4>, dim3(1), dim3(1024), np2 * 8, s, tokens, (int)n, np2, plan); break;
+    case 8: hipLaunchKernelGGL(embed_plan_kernel<8>, dim3(1), dim3(1024), np2 * 8, s, tokens, (int)n, np2, plan); break;
+    default: hipLaunchKernelGGL(embed_plan_kernel<16>, dim3(1), dim3(1024), np2 * 8, s, tokens, (int)n, np2, plan); break;
+  }
   MIT_LAUNCH_CHECK("mit_embed_plan");
   return MIT_OK;
 }

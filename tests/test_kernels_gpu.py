@@ -463,3 +463,27 @@ def test_gemm_grouped_folds_layernorm_param_grads():
         assert torch.equal(dg, rg) and torch.equal(db, rb)
     ref = A.double().cpu().t() @ B.double().cpu()
     assert (C.double().cpu() - ref).abs().max().item() < 1e-3 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("n", [1, 5, 1023, 1024, 1500, 4032, 9000, 16384])
+def test_embed_plan_matches_stable_sort(n):
+    """mit_embed_plan (register / shuffle / LDS bitonic stages): slot k holds the k-th position in
+    (token, position) order; plan[n + k] is the run length at a token's first slot, else 0."""
+    g = torch.Generator().manual_seed(n)
+    V = 50 if n > 64 else 7  # frequent repeats: long runs
+    tk = torch.randint(0, V, (n,), generator=g)
+    tk[:: max(1, n // 17)] = 3
+    plan = torch.empty(N.embed_plan_ints(n), dtype=torch.int32, device=dev())
+    N.embed_plan(tk.to(dev()), plan)
+    p = plan.cpu()
+    order = sorted(range(n), key=lambda i: (int(tk[i]), i))
+    assert p[:n].tolist() == order
+    runs = [0] * n
+    k = 0
+    while k < n:
+        j = k
+        while j < n and int(tk[order[j]]) == int(tk[order[k]]):
+            j += 1
+        runs[k] = j - k
+        k = j
+    assert p[n:].tolist() == runs
