@@ -118,6 +118,11 @@ int mit_gemm_set_variant(int variant);
 /* In-launch split-K combine (see workspace above): 0 = off (default; env MIT_GEMM_FUSED_SPLIT=1
  * seeds it on), 1 = on. A scheduling knob: results equal up to fp32 summation order. */
 int mit_gemm_set_fused_split(int on);
+/* Persistent 256x256 kernel for multi-round NT GEMMs with a gathered bf16 epilogue (one workgroup per
+ * CU walks its tiles; the next tile's first K-tile loads during this tile's epilogue): 0 = off
+ * (default; env MIT_G256_PERSIST=1 seeds it on), 1 = on. Bit-identical outputs; a scheduling knob
+ * (faster alone, slower beside concurrent streams: DESIGN.md §4.1e). */
+int mit_gemm_set_persist(int on);
 /* The launch mit_gemm would make for these args (no launch): returns the output tile edge of the
  * kernel (256 or 128 for bf16, 65 for the bf16 64x64 register-streaming kernel, 64 for the f32
  * kernel, 0 for an empty problem) and stores the

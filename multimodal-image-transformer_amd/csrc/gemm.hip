@@ -847,9 +847,18 @@ __device__ __forceinline__ void reg_epilogue(const f32x4 (&acc)[MI][4], const Ep
 // 5.9 -> 4.8 us; enc qkv+bias 51.1 -> 48.8 us, fc1 73.8 -> 68.8, kv_all 102 -> 94.7; residual loads as
 // 8-B segments in the accumulator layout instead: slower (o+res 28.6 -> 31.9 us). Image: row r at
 // r * 128 B, 16-B chunk c at (c ^ (r & 7)) * 16 (the 8-row x 8-chunk read-back is conflict-free).
-template <int ACT, bool DROP, bool XOPS>
+// PASSES = 2 (the persistent kernel): the 128 rows go through an 8 KiB image in two halves of 64 rows,
+// so half the LDS stays free for the next tile's first K-tile; after_loads() runs once the operand
+// loads have returned and before the first store (the persistent kernel issues that K-tile's DMA there).
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <int ACT, bool DROP, bool XOPS, int PASSES = 1, typename Hook = NoHook>
 __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const Epi& e, void* C, long ldc, long M,
-                                               long N, long mw, long nw, int lane, char* stg) {
+                                               long N, long mw, long nw, int lane, char* stg,
+                                               const Hook& after_loads = Hook{}) {
+  static_assert(PASSES == 1 || PASSES == 2, "stage_epilogue: 1 or 2 passes");
+  constexpr int IP = 8 / PASSES;  // 16-row blocks per pass
   const int g = lane >> 4, r16 = lane & 15;
   float bj[4][4];
 #pragma unroll
@@ -864,87 +873,92 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
   }
   typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
   const long cw = nw + 8 * (lane & 7);
+  // the residual / aux block arrives in whole-line loads (8 rows x 128 B per instruction, the store
+  // pattern) and is transposed to the accumulator layout through the same LDS image: each (i, j)
+  // segment is read back (ds_read_b64) right before the output segment overwrites it
+  u32x4 xl[XOPS ? 16 : 1];
   if constexpr (XOPS) {
-    // the residual / aux block arrives in whole-line loads (8 rows x 128 B per instruction, the store
-    // pattern) and is transposed to the accumulator layout through the same LDS image: each (i, j)
-    // segment is read back (ds_read_b64) right before the output segment overwrites it
     const bf16* src = (const bf16*)(e.res ? e.res : e.aux);
     const long ldx = e.res ? e.ldr : e.ld_aux;
-    u32x4 xl[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const long row = mw + 8 * q + (lane >> 3);
       xl[q] = (row < M && cw < N) ? *(const u32x4*)(src + row * ldx + cw) : u32x4{0u, 0u, 0u, 0u};
     }
-    gather_wait();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int rr = 8 * q + (lane >> 3);
-      *(u32x4*)(stg + rr * 128 + (((lane & 7) ^ (rr & 7)) << 4)) = xl[q];
-    }
-  } else {
-    gather_wait();
   }
+  gather_wait();
+  after_loads();
   const uint64_t key = epi_key<DROP>(e);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int rr = 16 * i + r16;
-    const long row = mw + rr;
+  for (int ps = 0; ps < PASSES; ++ps) {
+    if constexpr (XOPS) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float v[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t] * e.alpha + bj[j][t];
-      if (ACT == MIT_ACT_GELU) {
-#pragma unroll
-        for (int t = 0; t < 4; t += 2) {
-          const f32x2 q = gelu_fast2(f32x2{v[t], v[t + 1]});
-          v[t] = q[0];
-          v[t + 1] = q[1];
-        }
-      } else if (ACT != MIT_ACT_NONE) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = act_apply<ACT, true>(e.act, v[t]);
+      for (int q = 0; q < 16 / PASSES; ++q) {
+        const int rr = 8 * q + (lane >> 3);
+        *(u32x4*)(stg + rr * 128 + (((lane & 7) ^ (rr & 7)) << 4)) = xl[ps * (16 / PASSES) + q];
       }
-      const int ch = 2 * j + (g >> 1);
-      char* seg = stg + rr * 128 + ((ch ^ (rr & 7)) << 4) + (g & 1) * 8;
-      if constexpr (XOPS) {
-        const u32x2 x = *(const u32x2*)seg;
-        const float x0 = __uint_as_float(x[0] << 16), x1 = __uint_as_float(x[0] & 0xFFFF0000u);
-        const float x2 = __uint_as_float(x[1] << 16), x3 = __uint_as_float(x[1] & 0xFFFF0000u);
-        if (e.aux) {
-          v[0] *= x0 > 0.f ? e.aux_scale : 0.f;
-          v[1] *= x1 > 0.f ? e.aux_scale : 0.f;
-          v[2] *= x2 > 0.f ? e.aux_scale : 0.f;
-          v[3] *= x3 > 0.f ? e.aux_scale : 0.f;
+    }
+#pragma unroll
+    for (int ii = 0; ii < IP; ++ii) {
+      const int i = ps * IP + ii;
+      const int rr = 16 * ii + r16;  // row in the image
+      const long row = mw + 16 * i + r16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t] * e.alpha + bj[j][t];
+        if (ACT == MIT_ACT_GELU) {
+#pragma unroll
+          for (int t = 0; t < 4; t += 2) {
+            const f32x2 q = gelu_fast2(f32x2{v[t], v[t + 1]});
+            v[t] = q[0];
+            v[t + 1] = q[1];
+          }
+        } else if (ACT != MIT_ACT_NONE) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = act_apply<ACT, true>(e.act, v[t]);
         }
-        if (DROP && e.dropout) {
+        const int ch = 2 * j + (g >> 1);
+        char* seg = stg + rr * 128 + ((ch ^ (rr & 7)) << 4) + (g & 1) * 8;
+        if constexpr (XOPS) {
+          const u32x2 x = *(const u32x2*)seg;
+          const float x0 = __uint_as_float(x[0] << 16), x1 = __uint_as_float(x[0] & 0xFFFF0000u);
+          const float x2 = __uint_as_float(x[1] << 16), x3 = __uint_as_float(x[1] & 0xFFFF0000u);
+          if (e.aux) {
+            v[0] *= x0 > 0.f ? e.aux_scale : 0.f;
+            v[1] *= x1 > 0.f ? e.aux_scale : 0.f;
+            v[2] *= x2 > 0.f ? e.aux_scale : 0.f;
+            v[3] *= x3 > 0.f ? e.aux_scale : 0.f;
+          }
+          if (DROP && e.dropout) {
+            const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)(nw + 16 * j + 4 * g);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] *= drop_mul(key, base + t, e.thresh, e.dscale);
+          }
+          if (e.res) {
+            v[0] += x0;
+            v[1] += x1;
+            v[2] += x2;
+            v[3] += x3;
+          }
+        } else if (DROP && e.dropout) {
           const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)(nw + 16 * j + 4 * g);
 #pragma unroll
           for (int t = 0; t < 4; ++t) v[t] *= drop_mul(key, base + t, e.thresh, e.dscale);
         }
-        if (e.res) {
-          v[0] += x0;
-          v[1] += x1;
-          v[2] += x2;
-          v[3] += x3;
-        }
-      } else if (DROP && e.dropout) {
-        const uint64_t base = (uint64_t)row * (uint64_t)N + (uint64_t)(nw + 16 * j + 4 * g);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] *= drop_mul(key, base + t, e.thresh, e.dscale);
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        *(bf16x4*)seg = o;
       }
-      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-      const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      *(bf16x4*)seg = o;
     }
-  }
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int rr = 8 * q + (lane >> 3);
-    const u32x4 o = *(const u32x4*)(stg + rr * 128 + (((lane & 7) ^ (rr & 7)) << 4));
-    const long row = mw + rr;
-    if (row < M && cw < N) *(u32x4*)((bf16*)C + row * ldc + cw) = o;
+    for (int q = 0; q < 16 / PASSES; ++q) {
+      const int rr = 8 * q + (lane >> 3);
+      const u32x4 o = *(const u32x4*)(stg + rr * 128 + (((lane & 7) ^ (rr & 7)) << 4));
+      const long row = mw + 64 * ps + rr;
+      if (row < M && cw < N) *(u32x4*)((bf16*)C + row * ldc + cw) = o;
+    }
   }
 }
 
@@ -1379,6 +1393,172 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     }
     __builtin_amdgcn_wave_barrier();
   }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Persistent form of gemm256_kernel for multi-round NT grids (K-contig A and B, bf16 out, gathered
+// epilogue, an even number of 64-deep K-tiles): one workgroup per CU walks its tiles v, v + G, ...
+// (the same XCD-grouped order as the one-tile grid). Between two tiles the next tile's first K-tile
+// (buffer 0, free since K-tile nk-2) is DMA'd while this tile's epilogue runs -- its operand loads
+// return, the DMA goes out, then the stores -- with the epilogue staged through buffer 1 in two
+// 64-row passes. What it removes per tile after a workgroup's first: the ~2 us prologue (first
+// K-tile from L2 / HBM) and the dispatch gap of a new workgroup. Same K loop, same per-element MFMA
+// order and epilogue arithmetic as gemm256_kernel: bit-identical outputs.
+// ------------------------------------------------------------------------------------------------
+template <int ACT, bool DROP, int STG>
+__global__ __launch_bounds__(512) void gemm256p_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
+                                                       long M, long N, long K, long lda, long ldb, long ldc,
+                                                       int a_bytes, int b_bytes, Epi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int MI = 8, HR = 128, IH0 = 4, L = MIT_K_CONTIG;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nbn = (int)((N + B2 - 1) / B2), nbm = (int)((M + 255) / 256);
+  const int ntiles = nbn * nbm, G = (int)gridDim.x;
+  auto tile_of = [&](int v, long& m0, long& n0) {
+    const int bid = xcd_remap(v, ntiles);
+    const int GROUP = MIT_G256_GROUP;
+    const int first_m = (bid / (GROUP * nbn)) * GROUP;
+    const int gsize = min(nbm - first_m, GROUP);
+    m0 = (long)(first_m + (bid % (GROUP * nbn)) % gsize) * 256;
+    n0 = (long)((bid % (GROUP * nbn)) / gsize) * B2;
+  };
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
+  const int nk = (int)((K + BK - 1) / BK), klen = (int)K;
+  int v = blockIdx.x;
+  long m0, n0;
+  tile_of(v, m0, n0);
+  DmaPlan<L, HR> pa;
+  DmaPlan<L> pb;
+  pa.init(lda, M, m0, 0, wid, lane);
+  pb.init(ldb, N, n0, 0, wid, lane);
+  auto issue = [&](int X, int h, int t) -> bool {
+    if (t >= nk) return false;
+    char* dst = smem + (t & 1) * BUF_BYTES + (X * 2 + h) * HALF_BYTES + wid * 2048;
+    if (X == 0) pa.issue(ra, dst, h, t, klen);
+    else pb.issue(rb, dst, h, t, klen);
+    return true;
+  };
+  auto wait_dma = [&](bool younger_issued) {
+    if (younger_issued) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  f32x4 acc[MI][4];
+  bf16x8 af[IH0][2], blo[2][2], bhi[2][2];
+  auto read_a = [&](int buf, int ih) {
+    const char* base = smem + buf * BUF_BYTES + wr * HALF_BYTES;
+#pragma unroll
+    for (int i = 0; i < IH0; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag<L>(base, (ih * IH0 + i) * 16, kk, lane);
+  };
+  auto read_b = [&](int buf, int jh, bf16x8 (&bf)[2][2]) {
+    const char* base = smem + buf * BUF_BYTES + (2 + (wc >> 1)) * HALF_BYTES;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = frag<L>(base, (wc & 1) * 64 + jh * 32 + j * 16, kk, lane);
+  };
+  auto mma = [&](int ih, int jh, bf16x8 (&bf)[2][2]) {
+    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < IH0; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ih * IH0 + i][jh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[ih * IH0 + i][jh * 2 + j], 0, 0, 0);
+    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
+  // first tile's prologue: K-tile 0 (all four halves) and B0 of K-tile 1
+  issue(0, 0, 0);
+  issue(0, 1, 0);
+  issue(1, 0, 0);
+  issue(1, 1, 0);
+  wait_dma(issue(1, 0, 1));
+  bar_raw();
+  if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the K loop of gemm256_kernel (MIT_G256_PH4, early A1 DMA)
+    for (int t = 0; t < nk; t += 2) {
+      read_a(0, 0);
+      read_b(0, 0, blo);
+      issue(1, 1, t + 1);
+      read_b(0, 1, bhi);
+      issue(0, 0, t + 1);
+      issue(0, 1, t + 1);
+      bar_raw();
+      mma(0, 0, blo);
+      mma(0, 1, bhi);
+      bar_raw();
+
+      read_a(0, 1);
+      wait_dma(issue(1, 0, t + 2));
+      bar_raw();
+      mma(1, 1, bhi);
+      mma(1, 0, blo);
+      bar_raw();
+
+      read_a(1, 0);
+      read_b(1, 0, blo);
+      issue(1, 1, t + 2);
+      read_b(1, 1, bhi);
+      issue(0, 0, t + 2);
+      issue(0, 1, t + 2);
+      bar_raw();
+      mma(0, 0, blo);
+      mma(0, 1, bhi);
+      bar_raw();
+
+      read_a(1, 1);
+      wait_dma(issue(1, 0, t + 3));
+      // the epilogue stages into buffer 1 (the last K-tile's): its reads must have returned
+      if (t + 2 >= nk) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar_raw();
+      mma(1, 1, bhi);
+      mma(1, 0, blo);
+      if (!(wr == 1 && t + 2 >= nk)) bar_raw();  // the lagging group skips the last barrier
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int vn = v + G;
+    const bool more = vn < ntiles;
+    long m1 = 0, n1 = 0;
+    if (more) {
+      tile_of(vn, m1, n1);
+      pa.init(lda, M, m1, 0, wid, lane);
+      pb.init(ldb, N, n1, 0, wid, lane);
+    }
+    auto next_k0 = [&]() {  // the next tile's K-tile 0 into buffer 0 (last read at K-tile nk - 2)
+      if (more) {
+        issue(0, 0, 0);
+        issue(0, 1, 0);
+        issue(1, 0, 0);
+        issue(1, 1, 0);
+      }
+    };
+    // an opaque copy of the lane id: the epilogue's addresses are loop-invariant, and hoisted out of
+    // the tile loop they spilled (and their scratch reloads then waited behind the tile's stores)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    stage_epilogue<ACT, DROP, STG == 2, 2>(acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, ln,
+                                           smem + BUF_BYTES + wid * 8192, next_k0);
+    if (!more) break;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar_raw();  // every wave's image reads of buffer 1 returned: B0 of K-tile 1 may land there
+    wait_dma(issue(1, 0, 1));
+    bar_raw();
+    if (wr == 1) bar_raw();
+    v = vn;
+    m0 = m1;
+    n0 = n1;
   }
 }
 
@@ -1876,8 +2056,47 @@ void launch_rs(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, h
                      (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
 }
 
+int gemm_variant();
+int g_persist = -1;  // mit_gemm_set_persist; -1 = from env on first use
+// persistent 256 kernel (gemm256p_kernel): NT, gathered bf16 epilogue, more tiles than CUs, an even
+// K-tile count. Opt-in (MIT_G256_PERSIST=1; variant 8 forces the one-tile grid): alone it is 0-5 %
+// faster on the multi-round shapes (kv_all 93.1 -> 88.7 us, fc1+GELU 89.0 -> 86.9, CLIP-L o+res
+// 100.6 -> 103.9), but in the train step it is 9 % SLOWER (11605-11655 vs 12763-12806 pairs/s,
+// interleaved): a grid that holds every CU until its last tile starves the decoder's concurrent
+// kernels, which the one-tile grid lets in between tiles.
+template <int ACT, bool DROP>
+bool launch_256p(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  if (g_persist < 0) g_persist = getenv("MIT_G256_PERSIST") ? atoi(getenv("MIT_G256_PERSIST")) != 0 : 0;
+  const int on = g_persist;
+  const long tiles = ((g->M + 255) / 256) * ((g->N + B2 - 1) / B2), nk = (g->K + BK - 1) / BK;
+  const long G = (min((long)num_cus(), tiles) / 8) * 8;
+  if (!on || e.out_f32 || !epi_gatherable(e) || nk % 2 || G < 8 || tiles <= G) return false;
+  const bool ops = e.res || e.aux;
+  if (ops && ACT != MIT_ACT_NONE) return false;
+  static bool attr = false;
+  if (!attr) {
+    set_lds(gemm256p_kernel<ACT, DROP, 1>, SMEM2_BYTES);
+    if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256p_kernel<ACT, DROP, 2>, SMEM2_BYTES);
+    attr = true;
+  }
+  if constexpr (ACT == MIT_ACT_NONE) {
+    if (ops) {
+      hipLaunchKernelGGL((gemm256p_kernel<ACT, DROP, 2>), dim3((unsigned)G), dim3(512), SMEM2_BYTES, s,
+                         (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
+                         b_bytes, e);
+      return true;
+    }
+  }
+  hipLaunchKernelGGL((gemm256p_kernel<ACT, DROP, 1>), dim3((unsigned)G), dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+                     (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
+  return true;
+}
+
 template <int AL, int BL, int ACT, bool DROP, int MI>
 void launch_256_mi(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  if constexpr (MI == 8 && AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
+    if (gemm_variant() != 8 && launch_256p<ACT, DROP>(g, e, a_bytes, b_bytes, s)) return;
+  }
   const long nbm = (g->M + 32 * MI - 1) / (32 * MI), nbn = (g->N + B2 - 1) / B2;
   static bool attr = false;
   if (!attr) {
@@ -2019,7 +2238,7 @@ bool use_rs(const mit_gemm_args* g) {
 bool use_256(long M, long N, long K, int a_layout) {
   const int v = gemm_variant();
   if (v == 1) return false;
-  if (v == 2 || v == 5 || v == 6 || v == 7) return true;
+  if (v == 2 || v == 5 || v == 6 || v == 7 || v == 8) return true;
   // the MN-contig-A instances (weight gradients) exceed 256 VGPRs and spill: 128 kernel (+ split-K)
   if (a_layout != MIT_K_CONTIG) return false;
   if (M < 256 || N < 256 || K < 128) return false;
@@ -2135,8 +2354,14 @@ Split plan_split(const mit_gemm_args* g) {
 }  // namespace
 
 extern "C" int mit_gemm_set_variant(int v) {
-  MIT_CHECK_ARG((v >= 0 && v <= 3) || (v >= 5 && v <= 7), "mit_gemm_set_variant: %d not in {0,1,2,3,5,6,7}", v);
+  MIT_CHECK_ARG((v >= 0 && v <= 3) || (v >= 5 && v <= 8), "mit_gemm_set_variant: %d not in {0,1,2,3,5,6,7,8}", v);
   g_variant = v;
+  return MIT_OK;
+}
+
+extern "C" int mit_gemm_set_persist(int on) {
+  MIT_CHECK_ARG(on == 0 || on == 1, "mit_gemm_set_persist: %d not in {0,1}", on);
+  g_persist = on;
   return MIT_OK;
 }
 

@@ -79,6 +79,7 @@ SIGNATURES = {
     "mit_gemm_set_variant": (I, [I]),
     "mit_gemm_plan": (I, [ctypes.POINTER(GemmArgs), ctypes.POINTER(I)]),
     "mit_gemm_set_fused_split": (I, [I]),
+    "mit_gemm_set_persist": (I, [I]),
     "mit_gemm_grouped_ws_bytes": (L, [ctypes.POINTER(GemmArgs), I]),
     "mit_gemm_grouped": (I, [ctypes.POINTER(GemmArgs), I, ctypes.POINTER(LnGradsJob), I, vp, L, vp]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
@@ -475,6 +476,11 @@ def gemm_set_variant(v):
 def gemm_set_fused_split(on):
     """In-launch split-K combine for the <= 128-tile GEMMs (off by default)."""
     _check(lib().mit_gemm_set_fused_split(1 if on else 0), "mit_gemm_set_fused_split")
+
+
+def gemm_set_persist(on):
+    """Persistent 256x256 kernel for multi-round NT GEMMs (off by default: slower in the train step)."""
+    _check(lib().mit_gemm_set_persist(1 if on else 0), "mit_gemm_set_persist")
 
 
 def gemm_plan(g):

@@ -22,6 +22,7 @@ def _lib():
     yield
     N.gemm_set_variant(0)
     N.gemm_set_fused_split(0)
+    N.gemm_set_persist(0)
 
 
 def _ops(M, Nn, K, al, bl, seed=0):
@@ -273,3 +274,32 @@ def test_gemm_tall_race_screen():
         N.gemm(A, B, C, M, Nn, K)
         bad += int(not torch.equal(C, C0))
     assert bad == 0, f"{bad}/30 repeats differ bitwise (LDS race)"
+
+
+@pytest.mark.parametrize("M,Nn,K", [(4104, 4104, 768), (4352, 4096, 200), (12608, 2304, 768)])
+def test_gemm256_persistent_bit_identical(M, Nn, K):
+    """Multi-round NT grids run on the persistent 256 kernel (gemm256p_kernel: the next tile's first
+    K-tile loaded during this tile's two-pass staged epilogue); variant 8 forces the one-tile grid.
+    Same K loop and epilogue arithmetic: outputs bit-identical for every epilogue, and repeatable."""
+    A, B, ref = _ops(M, Nn, K, 0, 0, seed=8)
+    g = torch.Generator().manual_seed(9)
+    bias = torch.randn(Nn, generator=g).to(dev())
+    res = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
+    seed = torch.tensor([11], dtype=torch.int64, device=dev())
+    cases = [dict(), dict(bias=bias), dict(bias=bias, act=N.ACT_GELU), dict(residual=res, bias=bias),
+             dict(bias=bias, act=N.ACT_RELU, drop_p=0.1, seed=seed, site=3)]
+    N.gemm_set_persist(1)
+    for kw in cases:
+        outs = []
+        for v in (0, 8, 0):
+            N.gemm_set_variant(v)
+            C = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
+            N.gemm(A, B, C, M, Nn, K, **kw)
+            outs.append(C)
+        assert torch.equal(outs[0], outs[1]), (list(kw), (outs[0].float() - outs[1].float()).abs().max().item())
+        assert torch.equal(outs[0], outs[2])
+    N.gemm_set_persist(0)
+    N.gemm_set_variant(0)
+    C = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
+    N.gemm(A, B, C, M, Nn, K)
+    assert _rel(C, ref) < 8e-3
