@@ -350,7 +350,7 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
                                                long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
                                                int b_bytes, const Epi& e, int ksplit, long kchunk,
                                                float* __restrict__ ws, float* __restrict__ rowsum,
-                                               int* __restrict__ tile_cnt, long ws_bytes, int blk) {
+                                               int* __restrict__ tile_cnt, long ws_bytes, int blk, int GROUP = 8) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // NW = 4: waves 2 (M) x 2 (N), 64x64 each; NW = 8: 4 (M) x 2 (N), 32x64 each (MI 16-row blocks)
   constexpr int NT = 64 * NW, WR = 128 / (NW / 2), MI = WR / 16;
@@ -365,8 +365,8 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
   const int split = bid % ksplit;
   bid /= ksplit;
   const long kb = (long)split * kchunk, ke = min(K, kb + kchunk);
-  // groups of 8 M-blocks walk the N-blocks together (B panel reuse in L2)
-  const int GROUP = 8;
+  // groups of GROUP M-blocks walk the N-blocks together (B panel reuse in L2); GROUP = 1: row-major
+  // tiles, so an XCD's contiguous run of tiles shares its A row panels (the grouped dW launch)
   const int group_id = bid / (GROUP * nbn);
   const int first_m = group_id * GROUP;
   const int gsize = min(nbm - first_m, GROUP);
@@ -586,7 +586,7 @@ struct GroupLn {
 struct GroupArgs {
   GroupProb p[MAXG];
   GroupLn ln[MAXLN];
-  int n, nln, gemm_blocks;
+  int n, nln, gemm_blocks, group;
 };
 
 __device__ __forceinline__ void ln_grads_block(const GroupLn& j, int blk) {
@@ -622,9 +622,11 @@ __global__ __launch_bounds__(512) void gemm_bf16_grouped(GroupArgs ga) {
   int i = 0;
   while (i + 1 < ga.n && (int)blockIdx.x >= ga.p[i + 1].start) ++i;
   const GroupProb& q = ga.p[i];
+  // weight gradients dW = dY^T X with K = B*T: the dY column panel (K x 128, the A operand) of a
+  // tile row is read once when that row's tiles sit on one XCD (GROUP 1, MIT_GROUPED_GROUP)
   gemm_bf16_body<MIT_MN_CONTIG, MIT_MN_CONTIG, MIT_ACT_NONE, false, 2, 8>(
       q.A, q.B, q.C, q.M, q.N, q.K, q.lda, q.ldb, q.ldc, q.a_bytes, q.b_bytes, q.e, q.ksplit, q.kchunk, q.ws, q.rowsum,
-      nullptr, 0, (int)blockIdx.x - q.start);
+      nullptr, 0, (int)blockIdx.x - q.start, ga.group);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2526,6 +2528,8 @@ extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, const mit_ln_g
   const long s = grouped_split(tiles);
   GroupArgs ga;
   ga.n = n;
+  static const int grp = getenv("MIT_GROUPED_GROUP") ? atoi(getenv("MIT_GROUPED_GROUP")) : 1;
+  ga.group = grp > 0 ? grp : 1;
   int start = 0, rstart = 0;
   bool any_split = false;
   char* wsp = (char*)workspace + WS_HDR;

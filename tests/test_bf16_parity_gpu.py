@@ -7,10 +7,14 @@ the reference itself, in bf16, is 2.5e-2 .. 4.3e-2 off in max-abs on these fixtu
 so no bf16 implementation meets 1e-2 absolute; DESIGN.md §6 has the table. Bounds:
   logits   rel-L2 <= 1e-2 and <= 1.5x the reference-bf16 rel-L2; max-abs <= 1.5x the reference-bf16
            max-abs; argmax identical wherever the reference's top-1/top-2 margin > 5e-2
-  encoder  rel-L2 <= 2x the reference-bf16 encoder error (our residual stream is bf16, autocast's f32)
+  encoder  rel-L2 <= 1.75x the reference-bf16 encoder error (the 12-layer ViT towers keep a bf16
+           residual stream; autocast's is f32)
   step     loss within 5e-3, pre-clip grad norm within 1 %; per-tensor gradient error RMS / tensor RMS:
-           median <= 1.6x reference-bf16 + 0.01, worst tensor <= 2.5x reference-bf16's worst; every
-           tensor's norm within 10 %."""
+           median <= 1.4x reference-bf16 + 0.01, worst tensor <= 1.6x reference-bf16's worst; every
+           tensor's norm within 10 %.
+  The 24-layer CLIP-L configs (cfg2, cfg3: f32 encoder residual stream) are held tighter: logits
+  rel-L2 <= 8e-3, encoder <= 1.3x and worst gradient tensor <= 1.5x the reference's bf16 error
+  (measured round 3: 6.8e-3 / 7.4e-3, 1.00x / 0.98x, 1.05x / 1.22x; profiles/r03_bf16_parity.json)."""
 import json
 import os
 
@@ -43,9 +47,13 @@ def test_bf16_within_reference_bf16_envelope(name):
     assert r["logits_rel_l2"] <= 1.5 * c["logits_rel_l2"]
     assert r["logits_max_abs"] <= 1.5 * c["logits_max_abs"]
     assert r["argmax_agree_margin_gt_5e-2"] == 1.0
-    assert r["enc_rel_l2"] <= 2.0 * c["enc_rel_l2"]
+    assert r["enc_rel_l2"] <= 1.75 * c["enc_rel_l2"]
     assert r["step1_loss_abs_err"] <= 5e-3
     assert r["grad_norm_rel_err"] <= 1e-2
-    assert r["grad_rms_median"] <= 1.6 * c["grad_rms_median"] + 0.01
-    assert r["grad_rms_max"] <= 2.5 * c["grad_rms_max"]
+    assert r["grad_rms_median"] <= 1.4 * c["grad_rms_median"] + 0.01
+    assert r["grad_rms_max"] <= 1.6 * c["grad_rms_max"]
     assert r["grad_norm_rel_err_max"] <= 0.1
+    if name.startswith(("cfg2", "cfg3")):  # 24-layer CLIP-L towers, f32 encoder residual stream
+        assert r["logits_rel_l2"] <= 8e-3
+        assert r["enc_rel_l2"] <= 1.3 * c["enc_rel_l2"]
+        assert r["grad_rms_max"] <= 1.5 * c["grad_rms_max"]
