@@ -723,8 +723,15 @@ struct DmaPlan {
 #ifndef MIT_G256_REGEPI  // register epilogue in the one-tile 256 kernel (K-contig A)
 #define MIT_G256_REGEPI 1
 #endif
-#ifndef MIT_G256_PRIO  // raise the wave priority around each MFMA block
-#define MIT_G256_PRIO 1
+// Wave priority A/B (round 3, step A/B on one box): raising the priority around each MFMA
+// block (=1, round 2's default) and one static priority for the younger wave group
+// (MIT_G256_STATIC_PRIO) both measured 0.5 % slower in the step than no s_setprio at all with the
+// staged epilogue (12.42 k vs 12.49 k pairs/s, 3 alternations) -> off by default.
+#ifndef MIT_G256_PRIO
+#define MIT_G256_PRIO 0
+#endif
+#ifndef MIT_G256_STATIC_PRIO
+#define MIT_G256_STATIC_PRIO 0
 #endif
 // Epilogue staged through LDS (f32, two passes of 128 tile rows) so that every store instruction
 // writes MIT_G256_EPR whole rows of the tile (2: two 512-B row runs per wave instruction). The
@@ -1100,6 +1107,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   wait_dma(issue(1, 0, 1));
   bar_raw();
   if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
+#if MIT_G256_STATIC_PRIO  // A/B: one static priority for the younger half (guide: Two waves per SIMD, item 4)
+  if (wr == 1) __builtin_amdgcn_s_setprio(1);
+#endif
   G256_STAMP(2, __builtin_amdgcn_s_memtime());
 
 #if MIT_G256_PH4

@@ -5,7 +5,7 @@
 #   2) the same with --no-prefetch (encoder inline: per-kernel attribution without overlap)
 #   3) FETCH_SIZE and 4) WRITE_SIZE, each in its own pass (TCC slots; MI355X_MICROARCH.md HBM
 #      section) over the default command
-# Condense with tools/rocpd_summary.py into profiles/.
+# Condensed at the end (tools/rocpd_summary.py, tools/step_timeline.py) into $OUT/keep -> profiles/.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r03}
@@ -17,3 +17,16 @@ timeout -k 10 300 $P --kernel-trace --stats -d $OUT/trace -o run -- python3 benc
 timeout -k 10 300 $P --kernel-trace --stats -d $OUT/trace_noprefetch -o run -- python3 bench.py $ARGS --no-prefetch --no-roofline > $OUT/trace_noprefetch.json 2> $OUT/trace_noprefetch.err &&
 timeout -k 10 300 $P --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run -- python3 bench.py $ARGS --no-roofline > $OUT/fetch.json 2> $OUT/fetch.err &&
 timeout -k 10 300 $P --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o run -- python3 bench.py $ARGS --no-roofline > $OUT/write.json 2> $OUT/write.err
+# condense on the box (the rocpd databases exceed gpurun_out's copy-back cap): summaries under
+# $OUT/keep, databases deleted
+f() { find $OUT/$1 -name "$2" | head -n 1; }
+mkdir -p $OUT/keep &&
+python3 tools/rocpd_summary.py --trace $(f trace '*results.db') --fetch $(f fetch '*results.db') \
+  --write $(f write '*results.db') --trace-csv $(f trace '*kernel_trace.csv') --bench-json $OUT/trace.json \
+  --command "rocprofv3 --kernel-trace --stats / --pmc FETCH_SIZE / --pmc WRITE_SIZE -- python3 bench.py $ARGS" \
+  --out $OUT/keep/$TAG > $OUT/keep/summary.txt &&
+cp $(f trace '*kernel_stats.csv') $OUT/keep/${TAG}_bench_kernel_stats.csv &&
+cp $(f trace_noprefetch '*kernel_stats.csv') $OUT/keep/${TAG}_bench_noprefetch_kernel_stats.csv &&
+python3 tools/step_timeline.py $(f trace '*kernel_trace.csv') > $OUT/keep/${TAG}_step_breakdown.txt &&
+python3 tools/step_timeline.py $(f trace_noprefetch '*kernel_trace.csv') > $OUT/keep/${TAG}_step_breakdown_noprefetch.txt &&
+rm -rf $OUT/trace $OUT/trace_noprefetch $OUT/fetch $OUT/write
