@@ -504,6 +504,101 @@ __global__ __launch_bounds__(256) void ln_fwd_wide_kernel(long rows, long cols, 
   }
 }
 
+// Two rows per wave packed into whole 16-B chunks: a row of C = cols / 8 chunks, the wave's 2C chunks
+// spread over NV = 2C / 64 passes of all 64 lanes (cols 768: 3 passes, every lane busy; the one-row
+// form runs its second pass on half the lanes). Chunk j of the pair belongs to row j >= C; the two
+// rows' sums are two wave reductions over lane-selected partials. bf16 in / out.
+template <int NV, bool HASR>
+__global__ __launch_bounds__(256) void ln_fwd_pair_kernel(long rows, long cols, const bf16* x, long ldx,
+                                                          const bf16* __restrict__ r, long ldr, const uint64_t* seed,
+                                                          uint32_t site, uint32_t thresh, float dscale, int dropout,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, bf16* z, bf16* y,
+                                                          long ldy, float* mean, float* rstd) {
+  const int lane = threadIdx.x & 63;
+  const long C = cols >> 3;
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2;
+  const uint64_t key = dropout ? site_key(seed, site) : 0ull;
+  float v[NV][8];
+  bool hi[NV], ok[NV];
+  long cc[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const long j = i * 64 + lane;
+    hi[i] = j >= C;
+    cc[i] = (j - (hi[i] ? C : 0)) * 8;
+    const long row = row0 + (hi[i] ? 1 : 0);
+    ok[i] = row < rows;
+    float ra[HASR ? 8 : 1];
+    if (ok[i]) {
+      ld8(x + row * ldx + cc[i], v[i]);
+      if (HASR) ld8(r + row * ldr + cc[i], ra);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[i][k] = 0.f;
+    }
+    if (HASR && ok[i]) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float b = ra[k];
+        if (dropout) b *= drop_mul(key, (uint64_t)row * (uint64_t)cols + cc[i] + k, thresh, dscale);
+        v[i][k] += b;
+      }
+    }
+  }
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[i][k];
+    if (hi[i]) s1 += s;
+    else s0 += s;
+  }
+  const float inv = 1.f / (float)cols;
+  const float mu0 = wave_sum(s0) * inv, mu1 = wave_sum(s1) * inv;
+  float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float mu = hi[i] ? mu1 : mu0;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float d = v[i][k] - mu;
+      q += d * d;
+    }
+    if (hi[i]) q1 += q;
+    else q0 += q;
+  }
+  const float rs0 = rsqrtf(wave_sum(q0) * inv + eps), rs1 = rsqrtf(wave_sum(q1) * inv + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (!ok[i]) continue;
+    const long row = row0 + (hi[i] ? 1 : 0), c0 = cc[i];
+    const float mu = hi[i] ? mu1 : mu0, rs = hi[i] ? rs1 : rs0;
+    const f32x4 g0 = *(const f32x4*)(gamma + c0), g1 = *(const f32x4*)(gamma + c0 + 4);
+    const f32x4 b0 = *(const f32x4*)(beta + c0), b1 = *(const f32x4*)(beta + c0 + 4);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = (v[i][k] - mu) * rs * g0[k] + b0[k];
+      o[k + 4] = (v[i][k + 4] - mu) * rs * g1[k] + b1[k];
+    }
+    if (z) st8(z + row * cols + c0, v[i]);
+    st8(y + row * ldy + c0, o);
+  }
+  if (lane == 0) {
+    if (mean) {
+      if (row0 < rows) mean[row0] = mu0;
+      if (row0 + 1 < rows) mean[row0 + 1] = mu1;
+    }
+    if (rstd) {
+      if (row0 < rows) rstd[row0] = rs0;
+      if (row0 + 1 < rows) rstd[row0 + 1] = rs1;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x, long ldx, const void* r, long ldr,
@@ -535,6 +630,30 @@ extern "C" int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x,
     // 4032 x 512 + residual + dropout 6.3 / 6.5 / 8.7 us -- one row per wave: the most waves in flight
     static const int rw_env = getenv("MIT_LN_RW") ? atoi(getenv("MIT_LN_RW")) : 0;
     const int RWs = rw_env ? rw_env : 1;
+    // widths whose two rows fill whole 64-lane passes (256: 1 pass, 768: 3): two rows per wave
+    // (env MIT_LN_PAIR=0: the one-row form). Alone (tools/ln_bench.py, interleaved): 16384 x 256
+    // 6.1 vs 7.6-8.2 us, 12608 x 768 + residual + dropout (configs[3]'s decoder width) 18.3 vs
+    // 19.7-20.0 us; the encoder's 768-wide LayerNorm without residual is not faster (10.0 vs 9.9 us:
+    // x -> y alone copies in 6.2 us, the rest is per-row latency) and keeps the one-row form
+    static const int pair = getenv("MIT_LN_PAIR") ? atoi(getenv("MIT_LN_PAIR")) : 1;
+    if (pair && !rw_env && (cols == 256 || (cols == 768 && r))) {
+      const dim3 g2((unsigned)((rows + 7) / 8));
+      auto go = [&](auto nvc) {
+        constexpr int NVc = decltype(nvc)::value;
+        if (r)
+          hipLaunchKernelGGL((ln_fwd_pair_kernel<NVc, true>), g2, dim3(256), 0, s, rows, cols, (const bf16*)x, ldx,
+                             (const bf16*)r, ldr, seed, site, th, sc, dropout, gamma, beta, eps, (bf16*)z, (bf16*)y,
+                             ldy, mean, rstd);
+        else
+          hipLaunchKernelGGL((ln_fwd_pair_kernel<NVc, false>), g2, dim3(256), 0, s, rows, cols, (const bf16*)x, ldx,
+                             (const bf16*)r, ldr, seed, site, th, sc, dropout, gamma, beta, eps, (bf16*)z, (bf16*)y,
+                             ldy, mean, rstd);
+      };
+      if (cols == 256) go(std::integral_constant<int, 1>());
+      else go(std::integral_constant<int, 3>());
+      MIT_LAUNCH_CHECK("mit_layernorm_fwd");
+      return MIT_OK;
+    }
     auto launch = [&](auto nvc, auto rwc) {
       constexpr int NVc = decltype(nvc)::value, RWc = decltype(rwc)::value;
       const dim3 g2((unsigned)((rows + 4 * RWc - 1) / (4 * RWc)));

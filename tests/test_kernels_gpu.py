@@ -119,7 +119,7 @@ def test_dropout_mask_and_gemm_dropout():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("cols", [128, 192, 200, 130, 512, 768, 1024])
+@pytest.mark.parametrize("cols", [128, 192, 200, 130, 256, 512, 768, 1024])
 def test_layernorm_fwd_bwd(dtype, cols):
     rows = 200
     x = torch.randn(rows, cols, device=dev()).to(dtype)
@@ -155,6 +155,36 @@ def test_layernorm_fwd_bwd(dtype, cols):
     N.layernorm_bwd(dy, z, mean, rstd, g, dx2, None, None, ws2)
     N.layernorm_param_grads(rows, cols, ws2, dg2, db2)
     assert torch.equal(dx2, dx) and torch.equal(dg2, dg) and torch.equal(db2, db)
+
+
+@pytest.mark.parametrize("cols", [256, 768])
+@pytest.mark.parametrize("rows", [1, 3, 201, 12608])
+@pytest.mark.parametrize("res", [False, True])
+def test_layernorm_fwd_two_rows_per_wave(cols, rows, res):
+    """bf16 widths 256 / 768 run two rows per wave (ln_fwd_pair_kernel): odd row counts (the last
+    wave's second row out of range), statistics, residual with dropout, z written."""
+    x = torch.randn(rows, cols, device=dev()).to(torch.bfloat16)
+    g = 1 + 0.1 * torch.randn(cols, device=dev())
+    bta = 0.1 * torch.randn(cols, device=dev())
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(rows, device=dev()), torch.empty(rows, device=dev())
+    zr = x.float()
+    kw = {}
+    if res:
+        r = torch.randn(rows, cols, device=dev()).to(torch.bfloat16)
+        seed = torch.tensor([11], dtype=torch.int64, device=dev())
+        z = torch.empty_like(x)
+        kw = dict(r=r, drop_p=0.1, seed=seed, site=5, z=z)
+        mk = torch.empty(rows * cols, device=dev())
+        N.dropout_mask(rows * cols, 0.1, seed, 5, mk)
+        zr = zr + r.float() * mk.view(rows, cols)
+    N.layernorm_fwd(x, g, bta, 1e-5, y, mean=mean, rstd=rstd, **kw)
+    yr = F.layer_norm(zr, (cols,), g, bta, 1e-5)
+    _close(y, yr, 2e-2)
+    _close(mean, zr.mean(-1), 1e-5)
+    _close(rstd, torch.rsqrt(zr.var(-1, unbiased=False) + 1e-5), 1e-4)
+    if res:
+        _close(kw["z"], zr, 1e-2)
 
 
 def _attn_ref(q, k, v, causal, kpm, scale, drop=None):

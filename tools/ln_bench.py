@@ -10,7 +10,8 @@ import torch  # noqa: E402
 
 import native  # noqa: E402
 
-SHAPES = [("enc ln 768", 12608, 768, False), ("dec ln 512 +res+drop", 4032, 512, True), ("clip ln 1024", 36928, 1024, False)]
+SHAPES = [("enc ln 768", 12608, 768, False), ("enc ln 768 +res+drop", 12608, 768, True),
+          ("dec ln 512 +res+drop", 4032, 512, True), ("clip ln 1024", 36928, 1024, False), ("ln 256", 16384, 256, False)]
 
 
 def run(iters=50):
@@ -35,6 +36,14 @@ def run(iters=50):
         t = e0.elapsed_time(e1) / iters * 1e-3
         nb = R * C * 2 * (4 if res else 2)
         print(f"{name:22s} {R:6d} x {C:5d}  {t * 1e6:7.2f} us  {nb / t / 1e12:5.2f} TB/s", flush=True)
+        if not res:  # the same bytes as a plain device copy (x -> y), for scale
+            e0.record()
+            for _ in range(iters):
+                y.copy_(x)
+            e1.record()
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) / iters * 1e-3
+            print(f"{'  copy':22s} {R:6d} x {C:5d}  {t * 1e6:7.2f} us  {nb / t / 1e12:5.2f} TB/s", flush=True)
 
 
 if __name__ == "__main__":
