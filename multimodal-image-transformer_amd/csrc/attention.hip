@@ -469,6 +469,16 @@ constexpr int HK_MAX = 640;  // keys per head the LDS can hold (K + V = 256 B pe
 #define MIT_ATTN_LAZY 0
 #endif
 constexpr float LAZY_LOG2 = MIT_ATTN_LAZY;
+// diagnostic builds (wrong results): 1 = K/V staging only, 2 = no staging. ViT-B/16 MHSA: staging
+// alone 6.8-7.0 us (38.7 MB of K/V at ~5.6 TB/s), the sweep alone 22.2-22.4 us, both 26.9 us -- the
+// query sweep (VALU softmax + MFMA at 2 workgroups per CU), not the staging, bounds the kernel
+#ifndef MIT_ATTN_DIAG
+#define MIT_ATTN_DIAG 0
+#endif
+#ifndef MIT_ATTN_HS  // K/V staging: chunk rows per thread with their loads in flight together (4 vs 1,
+#define MIT_ATTN_HS 4  // tools/attn_bench.py: decoder cross 8.8 vs 9.4 us, ViT-B/16 and CLIP-L equal)
+#endif
+constexpr int HS = MIT_ATTN_HS;
 
 // cross-lane reductions over the 4 lane groups of a 16-query tile (lanes l, l ^ 16, l ^ 32, l ^ 48
 // hold one query's key groups): v_permlane16_swap / v_permlane32_swap of a value with itself leave
@@ -505,18 +515,31 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
   const bf16* Vb = (const bf16*)a.v + b * a.v_batch + h * D;
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, kbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, vbytes, 0x00020000);
-  // stage K and V: 8 16-B chunks per row
-  for (int id = tid; id < lkp * 8; id += blockDim.x) {
-    const int r = id >> 3, c = id & 7;
-    const bool ok = r < Lk;
-    const u32x4 kv = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   rk, (int)(ok ? (uint32_t)((r * a.k_row + c * 8) * 2) : A_OOB), 0, 0));
-    const u32x4 vv = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                   rv, (int)(ok ? (uint32_t)((r * a.v_row + c * 8) * 2) : A_OOB), 0, 0));
-    *(u32x4*)(Ks + koff_k(r, c)) = kv;
-    *(u32x4*)(Vs + koff_v(r, c * 16)) = vv;
+  // stage K and V: 8 16-B chunks per row, HS rows of chunks per thread with all their loads in flight
+  // before the first LDS write (one round trip per HS, not per chunk row)
+  const int nid = lkp * 8;
+  for (int base = tid; base < (MIT_ATTN_DIAG == 2 ? 0 : nid); base += HS * (int)blockDim.x) {
+    u32x4 kv[HS], vv[HS];
+#pragma unroll
+    for (int u = 0; u < HS; ++u) {
+      const int id = base + u * (int)blockDim.x, r = id >> 3, c = id & 7;
+      const bool ok = r < Lk;  // id >= nid gives r >= lkp >= Lk
+      kv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rk, (int)(ok ? (uint32_t)((r * a.k_row + c * 8) * 2) : A_OOB), 0, 0));
+      vv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rv, (int)(ok ? (uint32_t)((r * a.v_row + c * 8) * 2) : A_OOB), 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < HS; ++u) {
+      const int id = base + u * (int)blockDim.x, r = id >> 3, c = id & 7;
+      if (id < nid) {
+        *(u32x4*)(Ks + koff_k(r, c)) = kv[u];
+        *(u32x4*)(Vs + koff_v(r, c * 16)) = vv[u];
+      }
+    }
   }
   __syncthreads();
+  if (MIT_ATTN_DIAG == 1) return;  // diagnostic builds only (wrong results): staging alone
 
   const float sl2 = a.scale * 1.4426950408889634f;  // scores in log2 units
   const uint64_t key = DROP ? site_key(a.seed, a.site) : 0ull;
