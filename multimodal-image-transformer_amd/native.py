@@ -150,6 +150,24 @@ def lib() -> ctypes.CDLL:
     return _lib if _lib is not None else load_library()
 
 
+TORCH_OPS_PATH = os.path.join(_HERE, "lib", "libmit_torch_ops.so")
+_torch_ops_loaded = False
+
+
+def load_torch_ops(path: str = None):
+    """Register the dispatcher ops of csrc/torch_ops.cpp (TORCH_LIBRARY(mit_hip)): torch.ops.mit_hip.linear /
+    layer_norm / attention over the same kernels (the library links the in-tree libmit_hip.so). Device
+    tensors only: a CPU tensor has no kernel registered and the dispatcher raises. Returns torch.ops.mit_hip."""
+    global _torch_ops_loaded
+    if not _torch_ops_loaded:
+        p = path or TORCH_OPS_PATH
+        if not os.path.exists(p):
+            raise NativeError(f"libmit_torch_ops.so not found at {p}: build it with `python __graft_entry__.py build`")
+        torch.ops.load_library(p)
+        _torch_ops_loaded = True
+    return torch.ops.mit_hip
+
+
 def require_gpu():
     if not torch.cuda.is_available():
         raise NativeError("multimodal-image-transformer_amd kernels need a ROCm GPU (MI355X / gfx950); none is "
