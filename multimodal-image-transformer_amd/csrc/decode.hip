@@ -762,14 +762,17 @@ int launch_decode_gemm_nw(const mit_decode_gemm_args* g, hipStream_t s) {
   MIT_LAUNCH_CHECK("mit_decode_gemm");
   return MIT_OK;
 }
-// long K on a bf16 operand (linear2, K = d_ff): 8 waves split it over 32 x 64 tiles (twice the
-// blocks, a quarter of the K steps per wave: the K loop is one L2 round trip per step)
+// bf16 operand with K >= 512 (linear2 at K = d_ff, and since round 3 the K = 512 residual-LN GEMMs
+// self-out / cross-out): 8 waves split K over 32 x 64 tiles (twice the blocks, a quarter of the K
+// steps per wave: the K loop is one L2 round trip per step). Threshold 512 vs 1024 (env
+// MIT_DECODE_NW8_MINK): 782 vs 824 us per token step at B = 256, interleaved on one box
 int g_dg_long = -1;  // env MIT_DECODE_LONGK=0: 4 waves, 64-row tiles for every K (A/B)
 template <int AMODE, int ACT, int RMODE, bool CF32>
 int launch_decode_gemm(const mit_decode_gemm_args* g, hipStream_t s) {
   if (g_dg_long < 0) g_dg_long = getenv("MIT_DECODE_LONGK") ? atoi(getenv("MIT_DECODE_LONGK")) : 1;
+  static const long min_k = getenv("MIT_DECODE_NW8_MINK") ? atol(getenv("MIT_DECODE_NW8_MINK")) : 512;
   if constexpr (AMODE == 0) {
-    if (g_dg_long && g->K >= 1024) return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 8, 32>(g, s);
+    if (g_dg_long && g->K >= min_k) return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 8, 32>(g, s);
   }
   return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 4, 64>(g, s);
 }
