@@ -436,19 +436,21 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(mit_decode_gemm_ar
     const int a_bytes = (int)(2 * ((M - 1) * g.lda + K));
     ra = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, a_bytes, 0x00020000);
   } else {
-    static_assert(NW == 4 && BMR == 64, "LN-operand staging: 4 waves, 64 rows");
-    // wave w normalises rows 16w .. 16w+15; lane l owns columns 8l .. 8l+7 (+512 per pass). The
-    // first pass's z loads go out before the row statistics are merged (lanes 0-15 of the wave,
-    // one row each, shared by shuffles): one round trip, not two
+    // wave w normalises rows RPW*w .. RPW*w+RPW-1 (RPW = BMR / NW: 16 with 4 waves x 64 rows, 4 with
+    // 8 waves x 32 rows); lane l owns columns 8l .. 8l+7 (+512 per pass). The first pass's z loads go
+    // out before the row statistics are merged (lanes 0 .. RPW-1 of the wave, one row each, shared by
+    // shuffles): one round trip, not two
+    constexpr int RPW = BMR / NW;
+    static_assert(RPW * NW == BMR && RPW <= 16, "LN-operand staging: BMR / NW rows per wave");
     float mu_l = 0.f, rs_l = 0.f;
-    if (lane < 16 && m0 + w * 16 + lane < M)
-      dg_row_stats(g.a_stats + (m0 + w * 16 + lane) * 2 * ((K + 63) / 64), K, g.eps, mu_l, rs_l);
+    if (lane < RPW && m0 + w * RPW + lane < M)
+      dg_row_stats(g.a_stats + (m0 + w * RPW + lane) * 2 * ((K + 63) / 64), K, g.eps, mu_l, rs_l);
     for (long k = 8L * lane; k - 8L * lane < K; k += 512) {
       const bool kok = k < K;
-      f32x4 z[16][2];
+      f32x4 z[RPW][2];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int rr = w * 16 + i;
+      for (int i = 0; i < RPW; ++i) {
+        const int rr = w * RPW + i;
         if (kok && m0 + rr < M) {
           const float* zr = (const float*)g.A + (m0 + rr) * g.lda + k;
           z[i][0] = *(const f32x4*)zr;
@@ -460,8 +462,8 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(mit_decode_gemm_ar
       const f32x4 g0 = kok ? *(const f32x4*)(g.a_gamma + k) : f32x4{}, g1 = kok ? *(const f32x4*)(g.a_gamma + k + 4) : f32x4{};
       const f32x4 e0 = kok ? *(const f32x4*)(g.a_beta + k) : f32x4{}, e1 = kok ? *(const f32x4*)(g.a_beta + k + 4) : f32x4{};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int rr = w * 16 + i;
+      for (int i = 0; i < RPW; ++i) {
+        const int rr = w * RPW + i;
         const float mu = __shfl(mu_l, i, 64), rs = __shfl(rs_l, i, 64);
         bf16x8 o;
 #pragma unroll
@@ -751,7 +753,7 @@ template <int AMODE, int ACT, int RMODE, bool CF32, int NW, int BMR>
 int launch_decode_gemm_nw(const mit_decode_gemm_args* g, hipStream_t s) {
   const long nblk = ((g->M + BMR - 1) / BMR) * ((g->N + 63) / 64);
   const int red = NW * BMR * DG_RLD * 4;
-  const int lds = AMODE ? (int)max(64L * (g->K * 2 + 16), (long)red) : red;
+  const int lds = AMODE ? (int)max((long)BMR * (g->K * 2 + 16), (long)red) : red;
   static int attr = 0;
   if (attr < lds) {
     (void)hipFuncSetAttribute((const void*)decode_gemm_kernel<AMODE, ACT, RMODE, CF32, NW, BMR>,
@@ -771,8 +773,14 @@ template <int AMODE, int ACT, int RMODE, bool CF32>
 int launch_decode_gemm(const mit_decode_gemm_args* g, hipStream_t s) {
   if (g_dg_long < 0) g_dg_long = getenv("MIT_DECODE_LONGK") ? atoi(getenv("MIT_DECODE_LONGK")) : 1;
   static const long min_k = getenv("MIT_DECODE_NW8_MINK") ? atol(getenv("MIT_DECODE_NW8_MINK")) : 512;
+  // LN-operand GEMMs (in_proj, cross-q, linear1, head) on 8 waves x 32 rows as well (4 rows staged per
+  // wave): 782 -> 730 us per token step; env MIT_DECODE_LN8=0 keeps them on 4 waves x 64 rows, =N only
+  // up to N columns
+  static const long ln8 = getenv("MIT_DECODE_LN8") ? atol(getenv("MIT_DECODE_LN8")) : (1L << 40);
   if constexpr (AMODE == 0) {
     if (g_dg_long && g->K >= min_k) return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 8, 32>(g, s);
+  } else {
+    if (ln8 && g->N <= ln8) return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 8, 32>(g, s);
   }
   return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 4, 64>(g, s);
 }
