@@ -325,25 +325,37 @@ __global__ __launch_bounds__(256) void ce_rows_bf16(long rows, long V, bf16* log
     if (j < V) v[c] = *(const bf16x8*)(x + j);
   }
   const float xt = (!ign && tg >= 0 && tg < V) ? (float)x[tg] : 0.f;
+  // masked tail of a padded head: -inf (exp2 -> 0, max unaffected); whole 16-B chunks are in range
+  // (ld % 8 == 0), only the last may hold columns >= V
+#pragma unroll
+  for (int c = 0; c < CE_NCH; ++c) {
+    const long j = (long)c * 512 + lane * 8;
+    if (j < V && j + 8 > V) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (j + k >= V) v[c][k] = (bf16)(-INFINITY);
+    }
+  }
   float mx = -INFINITY;
 #pragma unroll
   for (int c = 0; c < CE_NCH; ++c) {
     const long j = (long)c * 512 + lane * 8;
     if (j < V) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (j + k < V) mx = fmaxf(mx, (float)v[c][k]);
+      for (int k = 0; k < 8; k += 2) mx = __builtin_fmaxf(mx, __builtin_fmaxf((float)v[c][k], (float)v[c][k + 1]));
     }
   }
   mx = wave_max(mx);
+  // exp(x - mx) as exp2(x log2e - mx log2e): one FMA + v_exp per element
+  constexpr float L2E = 1.4426950408889634f;
+  const float mxl = mx * L2E;
   float se = 0.f;
 #pragma unroll
   for (int c = 0; c < CE_NCH; ++c) {
     const long j = (long)c * 512 + lane * 8;
     if (j < V) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (j + k < V) se += __expf((float)v[c][k] - mx);
+      for (int k = 0; k < 8; ++k) se += __builtin_amdgcn_exp2f(fmaf((float)v[c][k], L2E, -mxl));
     }
   }
   se = wave_sum(se);
@@ -351,18 +363,23 @@ __global__ __launch_bounds__(256) void ce_rows_bf16(long rows, long V, bf16* log
   if (lane == 0) row_loss[row] = ign ? 0.f : lse - xt;
   if (!want_grad) return;
   const float gs = ign ? 0.f : 1.0f / *count;
-  const float inv = 1.0f / se;
+  // dlogit = gs * softmax - gs * [j == tg] = exp2(x log2e - (mx log2e + log2 se - log2 gs)) - gs [j == tg]
+  const float off = mxl + __log2f(se) - (gs > 0.f ? __log2f(gs) : 0.f);
 #pragma unroll
   for (int c = 0; c < CE_NCH; ++c) {
     const long j = (long)c * 512 + lane * 8;
     if (j < V) {
+      float q[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) q[k] = gs > 0.f ? __builtin_amdgcn_exp2f(fmaf((float)v[c][k], L2E, -off)) : 0.f;
+      if (tg >= j && tg < j + 8) {  // the target column (one lane of one chunk per row)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (j + k == tg) q[k] -= gs;
+      }
       bf16x8 o;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float p = __expf((float)v[c][k] - mx) * inv;
-        if (j + k == tg) p -= 1.0f;
-        o[k] = (j + k < V) ? (bf16)(p * gs) : (bf16)0.f;
-      }
+      for (int k = 0; k < 8; ++k) o[k] = (bf16)q[k];
       *(bf16x8*)(x + j) = o;
     }
   }
