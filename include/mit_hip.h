@@ -72,12 +72,9 @@ int mit_stream_wait_event(void* stream, void* event);
  *   rowsum (optional, f32 [M]): rowsum[m] = sum_k A(m,k) — the bias gradient when A = dY^T in a
  *     weight-gradient GEMM, fused in (no separate column-sum pass over dY).
  *   workspace: split-K scratch, size from mit_gemm_workspace_bytes(M, N, K); NULL / too small -> no
- *     split. Zero-fill it ONCE before first use: its first 4 KiB hold per-tile counters that every
- *     launch leaves at zero. One workspace per stream (launches sharing one must be ordered). Two
- *     split forms: plain-epilogue GEMMs with few output tiles and a long K (weight gradients) write
- *     fp32 partials and a second launch reduces them; with mit_gemm_set_fused_split(1), grids of
- *     <= 128 output tiles with any other epilogue but rowsum combine in-launch: the last K slice of
- *     a tile to finish sums the slabs in slice order and runs the epilogue (deterministic).
+ *     split. One workspace per stream (launches sharing one must be ordered). Plain-epilogue GEMMs with
+ *     few output tiles and a long K (weight gradients, the fc_out data gradient) write fp32 partials
+ *     and a second launch reduces them in slice order (deterministic).
  * bf16 requirements: lda, ldb and the contiguous extent of each operand multiples of 8; A, B 16-B aligned. */
 typedef struct {
   int dtype, a_layout, b_layout;
@@ -107,22 +104,11 @@ typedef struct {
 } mit_gemm_args;
 int mit_gemm(const mit_gemm_args* args, void* stream);
 long mit_gemm_workspace_bytes(long M, long N, long K);
-/* Tile-kernel choice for bf16 GEMMs: 0 = per shape (default; env MIT_GEMM_VARIANT seeds it),
- * 1 = 128x128 kernel only, 2 = 256x256 kernel wherever split-K is not planned, 3 = the 64x64
- * register-streaming kernel for every NT GEMM without rowsum / split-K, 5 / 6 = the 256-column
- * kernel with 160 / 192-row tiles wherever it applies (K-contig A, gatherable epilogue: bit-identical
- * to its 256-row tile; under 0 the 256-row tile, env MIT_G256_MI=5|6 forces a row count and -1 picks
- * per shape). Results are
- * identical up to fp32 summation order; a tuning / test knob, not a numerics switch. */
+/* Tile-kernel choice for bf16 GEMMs: 0 = per shape (default), 1 = 128x128 kernel only, 2 = 256x256
+ * kernel wherever split-K is not planned, 3 = the 64x64 register-streaming kernel for every NT GEMM
+ * without rowsum / split-K. Results are identical up to fp32 summation order; a test knob, not a
+ * numerics switch. */
 int mit_gemm_set_variant(int variant);
-/* In-launch split-K combine (see workspace above): 0 = off (default; env MIT_GEMM_FUSED_SPLIT=1
- * seeds it on), 1 = on. A scheduling knob: results equal up to fp32 summation order. */
-int mit_gemm_set_fused_split(int on);
-/* Persistent 256x256 kernel for multi-round NT GEMMs with a gathered bf16 epilogue (one workgroup per
- * CU walks its tiles; the next tile's first K-tile loads during this tile's epilogue): 0 = off
- * (default; env MIT_G256_PERSIST=1 seeds it on), 1 = on. Bit-identical outputs; a scheduling knob
- * (faster alone, slower beside concurrent streams: DESIGN.md §4.1e). */
-int mit_gemm_set_persist(int on);
 /* The launch mit_gemm would make for these args (no launch): returns the output tile edge of the
  * kernel (256 or 128 for bf16, 65 for the bf16 64x64 register-streaming kernel, 64 for the f32
  * kernel, 0 for an empty problem) and stores the

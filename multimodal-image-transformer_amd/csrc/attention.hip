@@ -1200,20 +1200,19 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
   const bool mfma_ok = Dh == D && dtype == MIT_BF16 && x->q_row % 8 == 0 && x->q_batch % 8 == 0 && x->k_row % 8 == 0 &&
                        x->k_batch % 8 == 0 && x->v_row % 8 == 0 && x->v_batch % 8 == 0 && x->o_row % 4 == 0 &&
                        x->o_batch % 4 == 0 && ((uintptr_t)x->q | (uintptr_t)x->k | (uintptr_t)x->v) % 16 == 0 &&
-                       ((uintptr_t)x->o % 8) == 0 && getenv("MIT_ATTN_SIMPLE") == nullptr;
-  static const int head_ok = getenv("MIT_ATTN_HEAD") ? atoi(getenv("MIT_ATTN_HEAD")) : 1;
+                       ((uintptr_t)x->o % 8) == 0;
   if (mfma_ok) {
     const long kb = 2 * ((Lk - 1) * x->k_row + D), vb = 2 * ((Lk - 1) * x->v_row + D);
     MIT_CHECK_ARG(kb < (1L << 31) && vb < (1L << 31), "mit_attention_fwd: K/V span >= 2 GiB");
-    if (head_ok && !a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535) {
+    if (!a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535) {
       // head-resident K/V: one workgroup per (b, h), NW waves balanced over the 16-query tiles.
       // K/V rows are staged to a multiple of 16 (the key tail of < 64 runs 16-key tiles: a ViT-B/16
-      // head of 197 keys sweeps 208 instead of 256; 28.5 -> 27.7 us, tools/gpu_ab.sh -m attn_bench.py MIT_ATTN_PAD=64 MIT_ATTN_PAD=16). <= 8 waves
+      // head of 197 keys sweeps 208 instead of 256; 28.5 -> 27.7 us, tools/attn_bench.py). <= 8 waves
       // whenever two heads fit the LDS, so a CU holds two workgroups and one stages its K/V while the
       // other computes. Three 5-wave workgroups per CU (one round of the 768 heads instead of 1.5,
       // 52 KiB each) measured slower (30.8 us): the CU's VALU, not the rounds, bounds this kernel.
-      // The dropout instance is built for <= 512 threads. MIT_ATTN_PAD=64 restores the round-1 staging.
-      static const int pad = getenv("MIT_ATTN_PAD") ? atoi(getenv("MIT_ATTN_PAD")) : 16;
+      // The dropout instance is built for <= 512 threads.
+      constexpr int pad = 16;
       const int lkp = (int)((Lk + pad - 1) / pad * pad);
       const int nqt = (int)((Lq + 15) / 16);
       const int maxw = (a.dropout || 2 * lkp * 256 <= 160 * 1024) ? 8 : 16;
@@ -1268,8 +1267,7 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
                        x->o_batch % 8 == 0 && gg->do_row % 8 == 0 && gg->do_batch % 8 == 0 && gg->dq_row % 4 == 0 &&
                        gg->dq_batch % 4 == 0 && gg->dk_row % 4 == 0 && gg->dk_batch % 4 == 0 && gg->dv_row % 4 == 0 &&
                        gg->dv_batch % 4 == 0 && al(x->q, 16) && al(x->k, 16) && al(x->v, 16) && al(x->o, 16) &&
-                       al(gg->dout, 16) && al(gg->dq, 8) && al(gg->dk, 8) && al(gg->dv, 8) &&
-                       getenv("MIT_ATTN_SIMPLE") == nullptr;
+                       al(gg->dout, 16) && al(gg->dq, 8) && al(gg->dk, 8) && al(gg->dv, 8);
   if (mfma_ok) {
     AttnBwdBytes nb;
     const long qb = 2 * ((Lq - 1) * x->q_row + D), kb = 2 * ((Lk - 1) * x->k_row + D);
@@ -1280,8 +1278,7 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
     nb.k = (int)kb;
     nb.v = (int)vb;
     nb.dO = (int)db;
-    static const int head_ok = getenv("MIT_ATTN_HEAD") ? atoi(getenv("MIT_ATTN_HEAD")) : 1;
-    if (head_ok && Lq <= 64 && Lk <= HB_MAXK && H <= 65535 && B <= 65535 && x->o_row % 8 == 0) {
+    if (Lq <= 64 && Lk <= HB_MAXK && H <= 65535 && B <= 65535 && x->o_row % 8 == 0) {
       const int lkp = (int)((Lk + 31) / 32 * 32);
       const int lds = 2 * lkp * 128 + 2 * 64 * 128 + 2 * 64 * 4;
       static bool attr = false;

@@ -667,9 +667,7 @@ extern "C" int mit_attention_decode(int dtype, long B, long H, long Dh, const vo
                     (v_row * esz) % 16 == 0 && (v_batch * esz) % 16 == 0 && (o_batch * esz) % 16 == 0,
                 "mit_attention_decode: rows must be 16-B aligned");
   if (B <= 0 || H <= 0) return MIT_OK;
-  static int rows = -1;  // env MIT_DECODE_ROWS_ATTN=0: the (b, h)-block kernel everywhere (A/B)
-  if (rows < 0) rows = getenv("MIT_DECODE_ROWS_ATTN") ? atoi(getenv("MIT_DECODE_ROWS_ATTN")) : 1;
-  if (rows && dtype == MIT_BF16 && H * Dh == 512 && B < (1L << 31)) {
+  if (dtype == MIT_BF16 && H * Dh == 512 && B < (1L << 31)) {
 #define MIT_ROWS_LAUNCH(DH_)                                                                                          \
   hipLaunchKernelGGL((attn_decode_rows_kernel<DH_, 8>), dim3((unsigned)B), dim3(512), 0, (hipStream_t)stream,         \
                      (const bf16*)q, q_batch, (const bf16*)k, k_row, k_batch, (const bf16*)v, v_row, v_batch, (bf16*)o, \
@@ -766,22 +764,12 @@ int launch_decode_gemm_nw(const mit_decode_gemm_args* g, hipStream_t s) {
 }
 // bf16 operand with K >= 512 (linear2 at K = d_ff, and since round 3 the K = 512 residual-LN GEMMs
 // self-out / cross-out): 8 waves split K over 32 x 64 tiles (twice the blocks, a quarter of the K
-// steps per wave: the K loop is one L2 round trip per step). Threshold 512 vs 1024 (env
-// MIT_DECODE_NW8_MINK): 782 vs 824 us per token step at B = 256, interleaved on one box
-int g_dg_long = -1;  // env MIT_DECODE_LONGK=0: 4 waves, 64-row tiles for every K (A/B)
+// steps per wave: the K loop is one L2 round trip per step). Threshold K >= 512 vs 1024: 782 vs 824 us
+// per token step at B = 256, interleaved on one box. The LN-operand GEMMs (in_proj, cross-q, linear1,
+// head) on 8 waves x 32 rows as well (4 rows staged per wave): 782 -> 730 us per token step.
 template <int AMODE, int ACT, int RMODE, bool CF32>
 int launch_decode_gemm(const mit_decode_gemm_args* g, hipStream_t s) {
-  if (g_dg_long < 0) g_dg_long = getenv("MIT_DECODE_LONGK") ? atoi(getenv("MIT_DECODE_LONGK")) : 1;
-  static const long min_k = getenv("MIT_DECODE_NW8_MINK") ? atol(getenv("MIT_DECODE_NW8_MINK")) : 512;
-  // LN-operand GEMMs (in_proj, cross-q, linear1, head) on 8 waves x 32 rows as well (4 rows staged per
-  // wave): 782 -> 730 us per token step; env MIT_DECODE_LN8=0 keeps them on 4 waves x 64 rows, =N only
-  // up to N columns
-  static const long ln8 = getenv("MIT_DECODE_LN8") ? atol(getenv("MIT_DECODE_LN8")) : (1L << 40);
-  if constexpr (AMODE == 0) {
-    if (g_dg_long && g->K >= min_k) return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 8, 32>(g, s);
-  } else {
-    if (ln8 && g->N <= ln8) return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 8, 32>(g, s);
-  }
+  if (AMODE != 0 || g->K >= 512) return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 8, 32>(g, s);
   return launch_decode_gemm_nw<AMODE, ACT, RMODE, CF32, 4, 64>(g, s);
 }
 }  // namespace

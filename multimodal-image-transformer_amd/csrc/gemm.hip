@@ -9,9 +9,9 @@
 //
 // Two bf16 tile kernels, fp32 accumulation on v_mfma_f32_16x16x32_bf16, both staging operands
 // HBM -> LDS by LDS-DMA (buffer_load ... lds) with the swizzle applied on the source address:
-//   * gemm_bf16_kernel: 128x128x64, 4 waves (2x2, 64x64 each), 2 blocks per CU, 2 LDS stages,
+//   * gemm_bf16_kernel: 128x128x64, 8 waves (4x2, 32x64 each), 2 blocks per CU, 2 LDS stages,
 //     optional split-K with fused bias-gradient row sums (weight gradients).
-//   * gemm256_kernel: 256x256x64, 8 waves (2x4, 128x64 each), 1 block per CU, 8-phase ping-pong
+//   * gemm256_kernel: 256x256x64, 8 waves (2x4, 128x64 each), 1 block per CU, 4-phase ping-pong
 //     schedule with half-tile DMA granularity and counted vmcnt (large GEMMs: the encoder's
 //     M = B*197 rows). mit_gemm picks per shape with an occupancy-quantised cost model.
 //   * K-contig tiles are XOR-swizzled for conflict-free ds_read_b128 fragment reads; MN-contig
@@ -234,9 +234,8 @@ __device__ __forceinline__ void epi8x(const Epi& e, void* C, long ldc, long N, l
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int TILE_BYTES = BM * BK * 2;          // 16 KiB per operand per stage
 constexpr int CST = BN + 4;                      // fp32 C-tile row stride in LDS (floats)
-// + 16 B past the fp32 C stage: the split-K combine's "last slice" flag
 constexpr int smem_bytes(int nst) {
-  return (2 * nst * TILE_BYTES > BM * CST * 4 + 16) ? 2 * nst * TILE_BYTES : BM * CST * 4 + 16;
+  return (2 * nst * TILE_BYTES > BM * CST * 4) ? 2 * nst * TILE_BYTES : BM * CST * 4;
 }
 constexpr uint32_t OOB = 0x80000000u;            // buffer offset past any num_records -> loads 0
 
@@ -349,8 +348,8 @@ template <int ALAY, int BLAY, int ACT, bool DROP, int NST, int NW>
 __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
                                                int b_bytes, const Epi& e, int ksplit, long kchunk,
-                                               float* __restrict__ ws, float* __restrict__ rowsum,
-                                               int* __restrict__ tile_cnt, long ws_bytes, int blk, int GROUP = 8) {
+                                               float* __restrict__ ws, float* __restrict__ rowsum, int blk,
+                                               int GROUP = 8) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // NW = 4: waves 2 (M) x 2 (N), 64x64 each; NW = 8: 4 (M) x 2 (N), 32x64 each (MI 16-row blocks)
   constexpr int NT = 64 * NW, WR = 128 / (NW / 2), MI = WR / 16;
@@ -361,7 +360,7 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
   const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
   int bid = xcd_remap(blk, nwg);
   // split-K: slice `split` covers k in [kb, ke); a tile's slices are neighbours in the remapped
-  // order, i.e. on one XCD (the in-launch combine below reads same-XCD slabs fastest)
+  // order, i.e. on one XCD
   const int split = bid % ksplit;
   bid /= ksplit;
   const long kb = (long)split * kchunk, ke = min(K, kb + kchunk);
@@ -463,38 +462,7 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
     }
   }
   __syncthreads();
-  // In-launch split-K combine (tile_cnt != NULL): every slice stores its fp32 partial tile as a
-  // write-through (sc1) slab, drains, and draws a ticket from the tile's counter; the slice that
-  // draws ksplit-1 acquires, sums the slabs in slice order (its own from LDS: the same bits) and
-  // runs the full epilogue, so the result does not depend on arrival order. It also re-zeroes the
-  // counter for the next launch (the caller zero-fills the workspace once).
-  if (tile_cnt) {
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)ws, (short)0, (int)ws_bytes, 0x00020000);
-    const int slab = (split * ntiles + bid) * (BM * BN);
-#pragma unroll 4
-    for (int pass = 0; pass < (BM * BN / 4) / NT; ++pass) {
-      const int id = pass * NT + tid;
-      const int r = id >> 5, c4 = (id & 31) * 4;
-      const f32x4 v = *(const f32x4*)(cs + r * CST + c4);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rw, (slab + r * BN + c4) * 4, 0, 16);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = (int*)(smem + BM * CST * 4);
-    if (tid == 0) {
-      const int t = __hip_atomic_fetch_add(tile_cnt + bid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = t == ksplit - 1;
-      if (last) {
-        __hip_atomic_store(tile_cnt + bid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      *flag = last;
-    }
-    __syncthreads();
-    if (!*flag) return;
-  }
-  if (!tile_cnt && ksplit == 1 && epi_gatherable(e)) {  // gathered epilogue: all loads, then all stores
+  if (ksplit == 1 && epi_gatherable(e)) {  // gathered epilogue: all loads, then all stores
     constexpr int NP = (BM * BN / 8) / NT;
     const long gc = n0 + (tid & 15) * 8;  // this thread's columns are the same in every pass
     float b[8];
@@ -521,22 +489,8 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
     const int r = id >> 4, c8 = (id & 15) * 8;
     const long gr = m0 + r, gc = n0 + c8;
     if (gr >= M || gc >= N) continue;
-    f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
-    if (tile_cnt) {
-      f32x4 sl = {0.f, 0.f, 0.f, 0.f}, sh = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < ksplit; ++k) {
-        if (k == split) {
-          sl += lo;
-          sh += hi;
-        } else {
-          const float* p = ws + (long)(k * ntiles + bid) * (BM * BN) + r * BN + c8;
-          sl += *(const f32x4*)p;
-          sh += *(const f32x4*)(p + 4);
-        }
-      }
-      lo = sl;
-      hi = sh;
-    } else if (ksplit > 1) {  // raw fp32 partial slab; gemm_splitk_reduce applies the (plain) epilogue
+    const f32x4 lo = *(const f32x4*)(cs + r * CST + c8), hi = *(const f32x4*)(cs + r * CST + c8 + 4);
+    if (ksplit > 1) {  // raw fp32 partial slab; gemm_splitk_reduce applies the (plain) epilogue
       f32x4* o = (f32x4*)(ws + ((long)split * M + gr) * N + gc);
       o[0] = lo;
       o[1] = hi;
@@ -547,14 +501,13 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
   }
 }
 
-template <int ALAY, int BLAY, int ACT, bool DROP, int NST, int NW = 4>
-__global__ __launch_bounds__(64 * NW) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
+template <int ALAY, int BLAY, int ACT, bool DROP>
+__global__ __launch_bounds__(512) void gemm_bf16_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                         long M, long N, long K, long lda, long ldb, long ldc,
                                                         int a_bytes, int b_bytes, Epi e, int ksplit, long kchunk,
-                                                        float* __restrict__ ws, float* __restrict__ rowsum,
-                                                        int* __restrict__ tile_cnt, long ws_bytes) {
-  gemm_bf16_body<ALAY, BLAY, ACT, DROP, NST, NW>(A, B, C, M, N, K, lda, ldb, ldc, a_bytes, b_bytes, e, ksplit, kchunk,
-                                                ws, rowsum, tile_cnt, ws_bytes, blockIdx.x);
+                                                        float* __restrict__ ws, float* __restrict__ rowsum) {
+  gemm_bf16_body<ALAY, BLAY, ACT, DROP, 2, 8>(A, B, C, M, N, K, lda, ldb, ldc, a_bytes, b_bytes, e, ksplit, kchunk, ws,
+                                             rowsum, blockIdx.x);
 }
 
 // Grouped weight-gradient GEMMs (dW = dY^T X, both operands MN-contig, f32 out, fused bias-gradient
@@ -623,10 +576,10 @@ __global__ __launch_bounds__(512) void gemm_bf16_grouped(GroupArgs ga) {
   while (i + 1 < ga.n && (int)blockIdx.x >= ga.p[i + 1].start) ++i;
   const GroupProb& q = ga.p[i];
   // weight gradients dW = dY^T X with K = B*T: the dY column panel (K x 128, the A operand) of a
-  // tile row is read once when that row's tiles sit on one XCD (GROUP 1, MIT_GROUPED_GROUP)
+  // tile row is read once when that row's tiles sit on one XCD (GROUP 1)
   gemm_bf16_body<MIT_MN_CONTIG, MIT_MN_CONTIG, MIT_ACT_NONE, false, 2, 8>(
       q.A, q.B, q.C, q.M, q.N, q.K, q.lda, q.ldb, q.ldc, q.a_bytes, q.b_bytes, q.e, q.ksplit, q.kchunk, q.ws, q.rowsum,
-      nullptr, 0, (int)blockIdx.x - q.start, ga.group);
+      (int)blockIdx.x - q.start, ga.group);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -704,83 +657,9 @@ struct DmaPlan {
   }
 };
 
-// compile-time A/B switches of the 256 kernel (tools/build_variants.sh): row-group height of the
-// tile order and the XCD remap
-#ifndef MIT_G256_GROUP
-#define MIT_G256_GROUP 4
-#endif
-#ifndef MIT_G256_NOREMAP
-#define MIT_G256_NOREMAP 0
-#endif
-// 4 barriers per K-tile (merged phases) with the A half-1 DMA issued one phase earlier is the
-// default (+3-5 % on the 256-tile shapes, profiles/r01_gemm256_schedule_ab.txt); 0 = the 8-phase loop
-#ifndef MIT_G256_PH4
-#define MIT_G256_PH4 1
-#endif
-#ifndef MIT_G256_EARLY_A1
-#define MIT_G256_EARLY_A1 1
-#endif
-#ifndef MIT_G256_REGEPI  // register epilogue in the one-tile 256 kernel (K-contig A)
-#define MIT_G256_REGEPI 1
-#endif
-// Wave priority A/B (round 3, step A/B on one box): raising the priority around each MFMA
-// block (=1, round 2's default) and one static priority for the younger wave group
-// (MIT_G256_STATIC_PRIO) both measured 0.5 % slower in the step than no s_setprio at all with the
-// staged epilogue (12.42 k vs 12.49 k pairs/s, 3 alternations) -> off by default.
-#ifndef MIT_G256_PRIO
-#define MIT_G256_PRIO 0
-#endif
-#ifndef MIT_G256_STATIC_PRIO
-#define MIT_G256_STATIC_PRIO 0
-#endif
-// Epilogue staged through LDS (f32, two passes of 128 tile rows) so that every store instruction
-// writes MIT_G256_EPR whole rows of the tile (2: two 512-B row runs per wave instruction). The
-// register epilogue's stores (16 rows x 64 B per instruction) and the 8-rows x 128-B form both run
-// at ~30 GB/s per CU (4.4-5 us per 256x256 bf16 tile, tools/g256_stamps.py), ~4x slower than
-// long contiguous runs: the store INSTRUCTION pattern, not bytes, bounds the epilogue.
-#ifndef MIT_G256_EPI_LDS
-#define MIT_G256_EPI_LDS 0
-#endif
-#ifndef MIT_G256_EPR
-#define MIT_G256_EPR 2
-#endif
-// bf16 outputs through each wave's private LDS stage (stage_epilogue) instead of the register
-// exchange (reg_epilogue)
-#ifndef MIT_G256_EPI_STAGE
-#define MIT_G256_EPI_STAGE 1
-#endif
-
-
-// Diagnostic build only (-DMIT_G256_STAMP, tools/g256_stamps.py): per workgroup, wave 0 and wave 4 stamp
-// the shader clock (s_memtime) at entry, after the prologue's first barrier, after the K loop and after
-// the epilogue's stores have drained, plus the 100 MHz global clock at entry / exit and the XCC id. The
-// stamps go to their own __device__ buffer (never an output); the shipped library compiles none of it.
-#ifdef MIT_G256_STAMP
-constexpr int G256_SLOTS = 24;  // wave 0: 0-5, wave 4: 6-11, 12 = exit global clock, 13/14 = stores issued, 15-22 epilogue steps (wave 0)
-__device__ unsigned long long g256_stamp[16384 * G256_SLOTS];
-#define G256_STAMP(slot, val)                                                                        \
-  do {                                                                                               \
-    if (lane == 0 && (wid == 0 || wid == 4) && blockIdx.x < 16384)                                   \
-      g256_stamp[blockIdx.x * G256_SLOTS + (slot) + (wid == 4 ? 6 : 0)] = (unsigned long long)(val); \
-  } while (0)
-__device__ __forceinline__ unsigned xcc_id() {
-  unsigned v;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-  return v & 15;
-}
-#define G256_STEP(slot)                                                                             \
-  do {                                                                                              \
-    if (lane == 0 && wid == 0 && blockIdx.x < 16384)                                                \
-      g256_stamp[blockIdx.x * G256_SLOTS + (slot)] = (unsigned long long)__builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define G256_STEP(slot) \
-  do {                  \
-  } while (0)
-#define G256_STAMP(slot, val) \
-  do {                        \
-  } while (0)
-#endif
+// tile order of the 256 kernel: XCD remap + groups of 4 row tiles walking the column tiles (row-group
+// heights 2 / 8 / 16 and no remap measured within +-1 %, profiles/r01_gemm256_tile_order_ab.txt)
+constexpr int G256_GROUP = 4;
 
 // Gathered register epilogue of one wave's (16 MI) x 64 output block, accumulated as C^T blocks
 // (MFMA operands swapped: lane holds row (lane & 15), columns 4 * (lane >> 4) + t of block j); rows
@@ -856,18 +735,10 @@ __device__ __forceinline__ void reg_epilogue(const f32x4 (&acc)[MI][4], const Ep
 // 5.9 -> 4.8 us; enc qkv+bias 51.1 -> 48.8 us, fc1 73.8 -> 68.8, kv_all 102 -> 94.7; residual loads as
 // 8-B segments in the accumulator layout instead: slower (o+res 28.6 -> 31.9 us). Image: row r at
 // r * 128 B, 16-B chunk c at (c ^ (r & 7)) * 16 (the 8-row x 8-chunk read-back is conflict-free).
-// PASSES = 2 (the persistent kernel): the 128 rows go through an 8 KiB image in two halves of 64 rows,
-// so half the LDS stays free for the next tile's first K-tile; after_loads() runs once the operand
-// loads have returned and before the first store (the persistent kernel issues that K-tile's DMA there).
-struct NoHook {
-  __device__ void operator()() const {}
-};
-template <int ACT, bool DROP, bool XOPS, int PASSES = 1, typename Hook = NoHook>
+template <int ACT, bool DROP, bool XOPS>
 __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const Epi& e, void* C, long ldc, long M,
-                                               long N, long mw, long nw, int lane, char* stg,
-                                               const Hook& after_loads = Hook{}) {
-  static_assert(PASSES == 1 || PASSES == 2, "stage_epilogue: 1 or 2 passes");
-  constexpr int IP = 8 / PASSES;  // 16-row blocks per pass
+                                               long N, long mw, long nw, int lane, char* stg) {
+  constexpr int PASSES = 1, IP = 8;  // one pass over the wave's 8 16-row blocks
   const int g = lane >> 4, r16 = lane & 15;
   float bj[4][4];
 #pragma unroll
@@ -896,7 +767,6 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
     }
   }
   gather_wait();
-  after_loads();
   const uint64_t key = epi_key<DROP>(e);
 #pragma unroll
   for (int ps = 0; ps < PASSES; ++ps) {
@@ -971,39 +841,25 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
   }
 }
 
-// MI = 16-row MFMA blocks per wave in M: 8 (256-row tiles) or 5 / 6 (160 / 192-row tiles, K-contig A
-// with the register epilogue only): the N = 768 / 1024 encoder GEMMs (o-proj, fc2) have 150 / 580
-// 256-row tiles -- one round on 150 of 256 CUs, or a third round for 68 tiles -- and shorter tiles fill
-// the rounds (mit_gemm picks per shape, tile_rounds_cost)
-template <int ALAY, int BLAY, int ACT, bool DROP, int MI = 8, int STG = 0>
+// STG (bf16 out, gathered epilogue, K-contig A): 1 = the LDS-staged epilogue without operands, 2 = with
+// the residual / aux block; 0 = the register (f32 out) or LDS-stage (MN-contig A) epilogue. A template
+// flag, not a run-time branch: two epilogues in one instance spill in the K loop.
+template <int ALAY, int BLAY, int ACT, bool DROP, int STG = 0>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
                                                       long M, long N, long K, long lda, long ldb, long ldc, int a_bytes,
-                                                      int b_bytes, Epi e, int ksplit, long kchunk,
-                                                      float* __restrict__ ws, float* __restrict__ rowsum) {
+                                                      int b_bytes, Epi e, float* __restrict__ ws,
+                                                      float* __restrict__ rowsum) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
-  static_assert(MI == 8 || (MI >= 4 && MI < 8 && ALAY == MIT_K_CONTIG), "gemm256_kernel: short tiles need K-contig A");
-#ifdef MIT_G256_STAMP
-  G256_STAMP(0, __builtin_amdgcn_s_memrealtime());
-  G256_STAMP(1, __builtin_amdgcn_s_memtime());
-  G256_STAMP(5, xcc_id());
-#endif
-  constexpr int HR = 16 * MI;          // rows per wave group = rows per A half-tile
-  constexpr int BMT = 2 * HR;          // tile rows
-  constexpr int IH0 = (MI + 1) / 2;    // row blocks in the wave's first row half (ih = 0)
+  (void)ws;
+  constexpr int MI = 8, HR = 128, BMT = 256, IH0 = 4;  // 16-row blocks per wave, rows per wave group / tile
 
   const int nbn = (int)((N + B2 - 1) / B2), nbm = (int)((M + BMT - 1) / BMT);
-  const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
-#if MIT_G256_NOREMAP
-  int bid = blockIdx.x;
-#else
-  int bid = xcd_remap(blockIdx.x, nwg);
-#endif
-  const int split = bid / ntiles;
-  bid -= split * ntiles;
-  const long kb = (long)split * kchunk, ke = min(K, kb + kchunk);
-  const int GROUP = MIT_G256_GROUP;
+  const int ntiles = nbn * nbm;
+  const int bid = xcd_remap(blockIdx.x, ntiles);
+  const long kb = 0, ke = K;
+  const int GROUP = G256_GROUP;
   const int group_id = bid / (GROUP * nbn);
   const int first_m = group_id * GROUP;
   const int gsize = min(nbm - first_m, GROUP);
@@ -1025,15 +881,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   // REG: accumulate C^T blocks (MFMA operands swapped: a lane holds 4 consecutive columns of one
   // row) so the epilogue can run from registers (no LDS stage, no barrier); used when the epilogue
   // is gatherable, else the C^T blocks are staged through LDS transposed
-  constexpr bool REG = ALAY == MIT_K_CONTIG && MIT_G256_REGEPI;
-  // LDS-staged row-run epilogue for every gatherable epilogue, else the register one
-  constexpr bool LDSEPI = REG && MIT_G256_EPI_LDS && MI == 8;
-  const bool ldsepi = LDSEPI && ksplit == 1 && epi_gatherable(e);
-  const bool regepi = REG && !ldsepi && ksplit == 1 && epi_gatherable(e);
-  // LDS-staged bf16 epilogue (stage_epilogue) for bf16 outputs of the 256-row tile
-  // STG (launch_256_mi, bf16 out): the LDS-staged epilogue, 1 = no operand, 2 = with the residual /
-  // aux operand. A template flag, not a run-time branch: two epilogues in one instance spill in the K loop
-  const bool stage = STG && MI == 8 && regepi;
+  constexpr bool REG = ALAY == MIT_K_CONTIG;
+  const bool regepi = REG && epi_gatherable(e);
+  const bool stage = STG && regepi;  // LDS-staged bf16 epilogue (stage_epilogue)
   float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   const int nk = (int)((ke - kb + BK - 1) / BK);
@@ -1051,13 +901,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     return true;
   };
   auto wait_dma = [&](bool younger_issued) {
-#ifdef MIT_G256_DIAG_NOWAIT  // timing diagnostic only (WRONG results): what the DMA waits cost
-    (void)younger_issued;
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-#else
     if (younger_issued) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
   };
 
   bf16x8 af[IH0][2], blo[2][2], bhi[2][2];
@@ -1069,7 +914,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
         if (i < ni) af[i][kk] = frag<ALAY>(base, (ih * IH0 + i) * 16, kk, lane);
-    if (TN && do_rs && MI == 8) {
+    if (TN && do_rs) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1085,7 +930,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   };
   auto mma = [&](int ih, int jh, bf16x8 (&bf)[2][2]) {
     const int ni = ih ? MI - IH0 : IH0;
-    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -1096,7 +940,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
             acc[ih * IH0 + i][jh * 2 + j] =
                 REG ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[ih * IH0 + i][jh * 2 + j], 0, 0, 0)
                     : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * IH0 + i][jh * 2 + j], 0, 0, 0);
-    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   // prologue: K-tile 0 (all four halves) and B0 of K-tile 1
@@ -1107,15 +950,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   wait_dma(issue(1, 0, 1));
   bar_raw();
   if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
-#if MIT_G256_STATIC_PRIO  // A/B: one static priority for the younger half (guide: Two waves per SIMD, item 4)
-  if (wr == 1) __builtin_amdgcn_s_setprio(1);
-#endif
-  G256_STAMP(2, __builtin_amdgcn_s_memtime());
 
-#if MIT_G256_PH4
-  // 4 barriers per K-tile instead of 8: the same reads, DMA issues and waits in the same order,
-  // two quarter-tile MFMA blocks per phase (a 512-cycle MFMA segment per group hides more of the
-  // other group's LDS-read latency)
+  // 4 barriers per K-tile (two quarter-tile MFMA blocks per phase: a 512-cycle MFMA segment per group
+  // hides more of the other group's LDS-read latency), every next-tile half-tile DMA issued in the
+  // first phase, one full MFMA block before its counted wait (+3-5 % on every 256-tile shape over
+  // the 8-phase loop, profiles/r01_gemm256_schedule_ab.txt)
   for (int t = 0; t < nk; t += 2) {
     const bool two = t + 1 < nk;
     read_a(0, 0);
@@ -1123,18 +962,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     issue(1, 1, t + 1);
     read_b(0, 1, bhi);
     issue(0, 0, t + 1);
-#if MIT_G256_EARLY_A1
     issue(0, 1, t + 1);
-#endif
     bar_raw();
     mma(0, 0, blo);
     mma(0, 1, bhi);
     bar_raw();
 
     read_a(0, 1);
-#if !MIT_G256_EARLY_A1
-    issue(0, 1, t + 1);
-#endif
     wait_dma(issue(1, 0, t + 2));
     bar_raw();
     mma(1, 1, bhi);
@@ -1148,9 +982,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     issue(1, 1, t + 2);
     if (two) read_b(1, 1, bhi);
     issue(0, 0, t + 2);
-#if MIT_G256_EARLY_A1
     issue(0, 1, t + 2);
-#endif
     bar_raw();
     if (two) {
       mma(0, 0, blo);
@@ -1159,9 +991,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     bar_raw();
 
     if (two) read_a(1, 1);
-#if !MIT_G256_EARLY_A1
-    issue(0, 1, t + 2);
-#endif
     wait_dma(issue(1, 0, t + 3));
     // staged epilogue: the lagging group writes its LDS stage into the last K-tile's buffer right after
     // its last MFMA block, so every wave's reads of that buffer must have RETURNED by this (for group 1:
@@ -1176,149 +1005,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     // LDS), so the leading group's epilogue overlaps its last MFMA block and neither waits
     if (!(regepi && wr == 1 && t + 2 >= nk)) bar_raw();  // (never skipped by the LDS-staged epilogue)
   }
-#else
-  for (int t = 0; t < nk; t += 2) {
-    const bool two = t + 1 < nk;  // second K-tile of this iteration exists
-    // ---- K-tile t (buffer 0) ----
-    read_a(0, 0);
-    read_b(0, 0, blo);
-    issue(1, 1, t + 1);
-    bar_raw();
-    mma(0, 0, blo);
-    bar_raw();
-
-    read_b(0, 1, bhi);
-    issue(0, 0, t + 1);
-    bar_raw();
-    mma(0, 1, bhi);
-    bar_raw();
-
-    read_a(0, 1);
-    issue(0, 1, t + 1);
-    bar_raw();
-    mma(1, 1, bhi);
-    bar_raw();
-
-    wait_dma(issue(1, 0, t + 2));
-    bar_raw();
-    mma(1, 0, blo);
-    bar_raw();
-
-    // ---- K-tile t+1 (buffer 1) ----
-    if (two) {
-      read_a(1, 0);
-      read_b(1, 0, blo);
-    }
-    issue(1, 1, t + 2);
-    bar_raw();
-    if (two) mma(0, 0, blo);
-    bar_raw();
-
-    if (two) read_b(1, 1, bhi);
-    issue(0, 0, t + 2);
-    bar_raw();
-    if (two) mma(0, 1, bhi);
-    bar_raw();
-
-    if (two) read_a(1, 1);
-    issue(0, 1, t + 2);
-    bar_raw();
-    if (two) mma(1, 1, bhi);
-    bar_raw();
-
-    wait_dma(issue(1, 0, t + 3));
-    bar_raw();
-    if (two) mma(1, 0, blo);
-    bar_raw();
-  }
-#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  G256_STAMP(3, __builtin_amdgcn_s_memtime());
-#ifdef MIT_G256_STAMP
-  struct StampEnd {  // stamps the epilogue's end (stores drained) on every return path
-    int lane, wid;
-    __device__ ~StampEnd() {
-      if (lane == 0 && (wid == 0 || wid == 4) && blockIdx.x < 16384)  // stores issued, not yet drained
-        g256_stamp[blockIdx.x * G256_SLOTS + 13 + (wid == 4)] = __builtin_amdgcn_s_memtime();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      G256_STAMP(4, __builtin_amdgcn_s_memtime());
-      if (wid == 0 && lane == 0 && blockIdx.x < 16384)
-        g256_stamp[blockIdx.x * G256_SLOTS + 12] = __builtin_amdgcn_s_memrealtime();
-    }
-  } stamp_end{lane, wid};
-#endif
-  if constexpr (LDSEPI) {
-    if (ldsepi) {
-      // Two passes over the accumulators: pass p stages row blocks i in [4p, 4p+4) of every wave
-      // (tile rows p*64 .. p*64+63 and 128+p*64 .. +63) as f32 in LDS ([128][256], 16-B chunks
-      // XOR-swizzled by row so the C^T-block writes are conflict-free), then every wave reads back
-      // whole-row runs and runs the same gathered epilogue (epi8x: identical arithmetic, bit-identical
-      // outputs) with its operands loaded in the same coalesced layout before any store.
-      constexpr int EPR = MIT_G256_EPR, LPR = 64 / EPR, CPI = 256 / (LPR * 8);
-      static_assert(EPR == 2 || EPR == 4 || EPR == 8, "MIT_G256_EPR: 2, 4 or 8 rows per store");
-      if (wr == 0) bar_raw();  // re-align the staggered groups: every LDS read of the loop is done
-      bar_raw();
-      G256_STEP(15);
-      auto lrow = [&](int q) { return wid * 16 + (q / CPI) * EPR + lane / LPR; };   // local row 0..127
-      auto lcol = [&](int q) { return (q % CPI) * (LPR * 8) + (lane % LPR) * 8; };  // tile column
-      auto grow = [&](int p, int q) {
-        const int lr = lrow(q);
-        return m0 + (lr >> 6) * 128 + p * 64 + (lr & 63);
-      };
-      auto chunk_off = [](int lr, int ch) { return lr * 1024 + ((ch ^ (lr & 7)) << 4); };
-      auto stage = [&](int p) {  // pass p's accumulators -> LDS (f32, C^T block: lane = row, 4 columns)
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int lr = wr * 64 + ii * 16 + (lane & 15);
-            const int ch = wc * 16 + j * 4 + (lane >> 4);
-            *(f32x4*)(smem + chunk_off(lr, ch)) = acc[p * 4 + ii][j];
-          }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        bar_raw();
-      };
-      auto fetch = [&](int q, float* v) {
-        const int lr = lrow(q), ch = lcol(q) >> 2;
-        const f32x4 a = *(const f32x4*)(smem + chunk_off(lr, ch)), b = *(const f32x4*)(smem + chunk_off(lr, ch + 1));
-        v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
-      };
-      float bq[CPI][8];
-#pragma unroll
-      for (int c = 0; c < CPI; ++c) epi_bias8(e, n0 + lcol(c), N, bq[c]);
-      const uint64_t key = epi_key<DROP>(e);
-      bf16x8 x0[8], x1[8];  // residual / aux segments of both passes, loaded before any store
-#pragma unroll
-      for (int q = 0; q < 8; ++q) x0[q] = epi_x8(e, M, N, grow(0, q), n0 + lcol(q));
-      stage(0);
-      G256_STEP(16);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) x1[q] = epi_x8(e, M, N, grow(1, q), n0 + lcol(q));
-      gather_wait();
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float v[8];
-        fetch(q, v);
-        const long gr = grow(0, q), gc = n0 + lcol(q);
-        if (gr < M && gc < N) epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v, bq[q % CPI], x0[q], key);
-      }
-      G256_STEP(17);
-      bar_raw();  // every wave's pass-0 reads are consumed (used above) before pass 1 overwrites LDS
-      G256_STEP(18);
-      stage(1);
-      G256_STEP(19);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float v[8];
-        fetch(q, v);
-        const long gr = grow(1, q), gc = n0 + lcol(q);
-        if (gr < M && gc < N) epi8x<ACT, DROP>(e, C, ldc, N, gr, gc, v, bq[q % CPI], x1[q], key);
-      }
-      return;
-    }
-  }
   if (regepi) {
-    if constexpr (MI == 8 && STG) {
+    if constexpr (STG) {
       if (stage) {
         // group 0 stages into the buffer NOT holding the last K-tile (its last reads were >= 2 phases
         // ago), group 1 into the last K-tile's buffer (every read of it returned by the last barrier)
@@ -1331,12 +1020,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
     reg_epilogue<ACT, DROP, MI>(acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane);
     return;
   }
-  if constexpr (MI == 8) {  // short tiles launch only with the register epilogue (launch_bf16_256)
   if (wr == 0) bar_raw();  // re-align the groups
   bar_raw();
 
   if (do_rs) {
-    float* dst = ksplit > 1 ? ws + (long)ksplit * M * N + (long)split * M : rowsum;
+    float* dst = rowsum;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float v = rs[i];
@@ -1349,7 +1037,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
 
   // ---- epilogue: per wave, two passes of 64 rows x 64 cols through a private fp32 LDS stage ----
   float* cs = (float*)smem + wid * 64 * EPI_LD;
-  const bool gather = ksplit == 1 && epi_gatherable(e);
+  const bool gather = epi_gatherable(e);
   const long gcw = n0 + wc * 64 + (lane & 7) * 8;  // this lane's columns in every pass / row
   float bw[8];
   uint64_t key = 0;
@@ -1394,326 +1082,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
       const long gr = m0 + wr * 128 + pass * 64 + r, gc = n0 + wc * 64 + c8;
       if (gr >= M || gc >= N) continue;
       const f32x4 lo = *(const f32x4*)(cs + r * EPI_LD + c8), hi = *(const f32x4*)(cs + r * EPI_LD + c8 + 4);
-      if (ksplit > 1) {
-        f32x4* o = (f32x4*)(ws + ((long)split * M + gr) * N + gc);
-        o[0] = lo;
-        o[1] = hi;
-        continue;
-      }
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       epi_row8<ACT, DROP>(e, C, ldc, N, gr, gc, v);
     }
     __builtin_amdgcn_wave_barrier();
   }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Persistent form of gemm256_kernel for multi-round NT grids (K-contig A and B, bf16 out, gathered
-// epilogue, an even number of 64-deep K-tiles): one workgroup per CU walks its tiles v, v + G, ...
-// (the same XCD-grouped order as the one-tile grid). Between two tiles the next tile's first K-tile
-// (buffer 0, free since K-tile nk-2) is DMA'd while this tile's epilogue runs -- its operand loads
-// return, the DMA goes out, then the stores -- with the epilogue staged through buffer 1 in two
-// 64-row passes. What it removes per tile after a workgroup's first: the ~2 us prologue (first
-// K-tile from L2 / HBM) and the dispatch gap of a new workgroup. Same K loop, same per-element MFMA
-// order and epilogue arithmetic as gemm256_kernel: bit-identical outputs.
-// ------------------------------------------------------------------------------------------------
-template <int ACT, bool DROP, int STG>
-__global__ __launch_bounds__(512) void gemm256p_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
-                                                       long M, long N, long K, long lda, long ldb, long ldc,
-                                                       int a_bytes, int b_bytes, Epi e) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int MI = 8, HR = 128, IH0 = 4, L = MIT_K_CONTIG;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  const int nbn = (int)((N + B2 - 1) / B2), nbm = (int)((M + 255) / 256);
-  const int ntiles = nbn * nbm, G = (int)gridDim.x;
-  auto tile_of = [&](int v, long& m0, long& n0) {
-    const int bid = xcd_remap(v, ntiles);
-    const int GROUP = MIT_G256_GROUP;
-    const int first_m = (bid / (GROUP * nbn)) * GROUP;
-    const int gsize = min(nbm - first_m, GROUP);
-    m0 = (long)(first_m + (bid % (GROUP * nbn)) % gsize) * 256;
-    n0 = (long)((bid % (GROUP * nbn)) / gsize) * B2;
-  };
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
-  const int nk = (int)((K + BK - 1) / BK), klen = (int)K;
-  int v = blockIdx.x;
-  long m0, n0;
-  tile_of(v, m0, n0);
-  DmaPlan<L, HR> pa;
-  DmaPlan<L> pb;
-  pa.init(lda, M, m0, 0, wid, lane);
-  pb.init(ldb, N, n0, 0, wid, lane);
-  auto issue = [&](int X, int h, int t) -> bool {
-    if (t >= nk) return false;
-    char* dst = smem + (t & 1) * BUF_BYTES + (X * 2 + h) * HALF_BYTES + wid * 2048;
-    if (X == 0) pa.issue(ra, dst, h, t, klen);
-    else pb.issue(rb, dst, h, t, klen);
-    return true;
-  };
-  auto wait_dma = [&](bool younger_issued) {
-    if (younger_issued) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-  f32x4 acc[MI][4];
-  bf16x8 af[IH0][2], blo[2][2], bhi[2][2];
-  auto read_a = [&](int buf, int ih) {
-    const char* base = smem + buf * BUF_BYTES + wr * HALF_BYTES;
-#pragma unroll
-    for (int i = 0; i < IH0; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag<L>(base, (ih * IH0 + i) * 16, kk, lane);
-  };
-  auto read_b = [&](int buf, int jh, bf16x8 (&bf)[2][2]) {
-    const char* base = smem + buf * BUF_BYTES + (2 + (wc >> 1)) * HALF_BYTES;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[j][kk] = frag<L>(base, (wc & 1) * 64 + jh * 32 + j * 16, kk, lane);
-  };
-  auto mma = [&](int ih, int jh, bf16x8 (&bf)[2][2]) {
-    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < IH0; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[ih * IH0 + i][jh * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], acc[ih * IH0 + i][jh * 2 + j], 0, 0, 0);
-    if (MIT_G256_PRIO) __builtin_amdgcn_s_setprio(0);
-  };
-
-  // first tile's prologue: K-tile 0 (all four halves) and B0 of K-tile 1
-  issue(0, 0, 0);
-  issue(0, 1, 0);
-  issue(1, 0, 0);
-  issue(1, 1, 0);
-  wait_dma(issue(1, 0, 1));
-  bar_raw();
-  if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
-  for (;;) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // the K loop of gemm256_kernel (MIT_G256_PH4, early A1 DMA)
-    for (int t = 0; t < nk; t += 2) {
-      read_a(0, 0);
-      read_b(0, 0, blo);
-      issue(1, 1, t + 1);
-      read_b(0, 1, bhi);
-      issue(0, 0, t + 1);
-      issue(0, 1, t + 1);
-      bar_raw();
-      mma(0, 0, blo);
-      mma(0, 1, bhi);
-      bar_raw();
-
-      read_a(0, 1);
-      wait_dma(issue(1, 0, t + 2));
-      bar_raw();
-      mma(1, 1, bhi);
-      mma(1, 0, blo);
-      bar_raw();
-
-      read_a(1, 0);
-      read_b(1, 0, blo);
-      issue(1, 1, t + 2);
-      read_b(1, 1, bhi);
-      issue(0, 0, t + 2);
-      issue(0, 1, t + 2);
-      bar_raw();
-      mma(0, 0, blo);
-      mma(0, 1, bhi);
-      bar_raw();
-
-      read_a(1, 1);
-      wait_dma(issue(1, 0, t + 3));
-      // the epilogue stages into buffer 1 (the last K-tile's): its reads must have returned
-      if (t + 2 >= nk) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      bar_raw();
-      mma(1, 1, bhi);
-      mma(1, 0, blo);
-      if (!(wr == 1 && t + 2 >= nk)) bar_raw();  // the lagging group skips the last barrier
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int vn = v + G;
-    const bool more = vn < ntiles;
-    long m1 = 0, n1 = 0;
-    if (more) {
-      tile_of(vn, m1, n1);
-      pa.init(lda, M, m1, 0, wid, lane);
-      pb.init(ldb, N, n1, 0, wid, lane);
-    }
-    auto next_k0 = [&]() {  // the next tile's K-tile 0 into buffer 0 (last read at K-tile nk - 2)
-      if (more) {
-        issue(0, 0, 0);
-        issue(0, 1, 0);
-        issue(1, 0, 0);
-        issue(1, 1, 0);
-      }
-    };
-    // an opaque copy of the lane id: the epilogue's addresses are loop-invariant, and hoisted out of
-    // the tile loop they spilled (and their scratch reloads then waited behind the tile's stores)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    stage_epilogue<ACT, DROP, STG == 2, 2>(acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, ln,
-                                           smem + BUF_BYTES + wid * 8192, next_k0);
-    if (!more) break;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    bar_raw();  // every wave's image reads of buffer 1 returned: B0 of K-tile 1 may land there
-    wait_dma(issue(1, 0, 1));
-    bar_raw();
-    if (wr == 1) bar_raw();
-    v = vn;
-    m0 = m1;
-    n0 = n1;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// bf16 MFMA kernel, 256x128 block tile, TWO workgroups per CU (NT: both operands K-contig; the
-// encoder's GEMMs and the decoder's kv_all / fc_out).
-//
-// Why: the 256x256 kernel's epilogue is a per-CU store stream (~11 B per clock per CU: a K = 768
-// tile spends 6-10 us of its 25-29 us writing 128 KiB, tools/g256_stamps.py), and with one
-// workgroup per CU nothing computes meanwhile. Here each CU holds two 4-wave workgroups (72 KiB LDS,
-// <= 256 VGPRs each), so one workgroup's prologue / epilogue runs beside the other's K loop and the
-// ping-pong of the 256 kernel's wave groups comes from the two workgroups instead of a schedule.
-//
-// 4 waves as 2 (M) x 2 (N), 128x64 each (8x4 accumulators, C^T blocks -> register epilogue). K in
-// steps of 32: three LDS stages of 24 KiB (A 256 x 32, B 128 x 32, 64-B rows), filled by LDS-DMA
-// two steps ahead (6 pieces per wave per stage), one barrier per step:
-//   wait vmcnt(6) (this wave's pieces of stage t landed, stage t+1's in flight) -> barrier (every
-//   wave's pieces of t landed; every wave's reads of step t-1 done) -> DMA stage t+2 into the slot of
-//   t-1 -> fragment reads of t -> 32 MFMAs.
-// ------------------------------------------------------------------------------------------------
-constexpr int T2_BK = 32;
-constexpr int T2_A_BYTES = 256 * T2_BK * 2;          // 16 KiB
-constexpr int T2_STAGE = T2_A_BYTES + 128 * T2_BK * 2;  // + B 8 KiB = 24 KiB
-constexpr int T2_NST = 3;
-constexpr int T2_SMEM = T2_NST * T2_STAGE;            // 72 KiB: two workgroups per CU
-#ifndef MIT_GT_GROUP
-#define MIT_GT_GROUP 4
-#endif
-// 16-B chunk c (0..3) of row r in a [rows][32] bf16 image (64-B rows). The chunks of rows 8-15 of
-// every 16-row fragment are XOR 3: the four lane groups of a ds_read_b128 ({0-3,12-15,20-27}, ...)
-// then each cover all 64 banks once (conflict-free fragment reads).
-__device__ __forceinline__ int t2off(int r, int c) { return r * 64 + ((c ^ (((r >> 3) & 1) * 3)) << 4); }
-
-template <int ACT, bool DROP>
-__global__ __launch_bounds__(256, 2) void gemm_tall_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                           void* C, long M, long N, long K, long lda, long ldb, long ldc,
-                                                           int a_bytes, int b_bytes, Epi e) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int nbn = (int)((N + 127) / 128), nbm = (int)((M + 255) / 256);
-  const int ntiles = nbn * nbm;
-  const int bid = xcd_remap(blockIdx.x, ntiles);
-  const int GROUP = MIT_GT_GROUP;  // row groups of GROUP M-tiles walk the N-tiles together (L2 reuse)
-  const int group_id = bid / (GROUP * nbn);
-  const int first_m = group_id * GROUP;
-  const int gsize = min(nbm - first_m, GROUP);
-  const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
-  const int bn = (bid % (GROUP * nbn)) / gsize;
-  const long m0 = (long)bm * 256, n0 = (long)bn * 128;
-
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
-
-  // LDS-DMA plan: piece p (1 KiB = 16 rows x 64 B) of the A image is issued by wave p / 4, of the B
-  // image by wave p / 2; lane l fills row 16p + l / 4, physical chunk l % 4 = logical chunk c ^ swz
-  uint32_t abase[4], bbase[2];
-  int akc[4], bkc[2];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r = (wid * 4 + j) * 16 + (lane >> 2), c = (lane & 3) ^ (((r >> 3) & 1) * 3);
-    akc[j] = c * 8;
-    abase[j] = m0 + r < M ? (uint32_t)(((m0 + r) * lda + c * 8) * 2) : OOB;
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = (wid * 2 + j) * 16 + (lane >> 2), c = (lane & 3) ^ (((r >> 3) & 1) * 3);
-    bkc[j] = c * 8;
-    bbase[j] = n0 + r < N ? (uint32_t)(((n0 + r) * ldb + c * 8) * 2) : OOB;
-  }
-  const int nk = (int)((K + T2_BK - 1) / T2_BK);
-  auto issue = [&](int t) {
-    char* st = smem + (t % T2_NST) * T2_STAGE;
-    const uint32_t koff = (uint32_t)t * (T2_BK * 2);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t boff = (t * T2_BK + akc[j] < K) ? abase[j] + koff : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(st + (wid * 4 + j) * 1024),
-                                               16, boff, 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const uint32_t boff = (t * T2_BK + bkc[j] < K) ? bbase[j] + koff : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rb, (__attribute__((address_space(3))) void*)(st + T2_A_BYTES + (wid * 2 + j) * 1024), 16, boff, 0, 0, 0);
-    }
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // fragment read offsets inside a stage: A row block i of this wave, B column block j
-  const int aoff = t2off(wr * 128 + (lane & 15), lane >> 4);
-  const int boff0 = T2_A_BYTES + t2off(wc * 64 + (lane & 15), lane >> 4);
-
-  // Software pipeline: the fragments of step t+1 are read while step t's MFMAs run (two register
-  // sets, the loop unrolled by two so both are statically named). Step t: wait for this wave's
-  // pieces of stage t+1 and its own reads of stage t -> barrier (stage t+1 visible to all; every
-  // wave's stage-t fragments are in registers, so slot t is free) -> DMA stage t+3 into slot t ->
-  // read stage t+1 -> MFMAs of t. Three slots: t+1 (read now), t+2 (in flight), t+3 (issued now).
-  auto wait_next = [&](int t) {  // this wave's pieces of stage t+1 landed (t+2, if any, may fly)
-    if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  };
-  auto read = [&](int t, bf16x8 (&af)[8], bf16x8 (&bfr)[4]) {
-    const char* st = smem + (t % T2_NST) * T2_STAGE;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = __builtin_bit_cast(bf16x8, *(const u32x4*)(st + boff0 + j * 1024));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = __builtin_bit_cast(bf16x8, *(const u32x4*)(st + aoff + i * 1024));
-  };
-  auto mma = [&](const bf16x8 (&af)[8], const bf16x8 (&bfr)[4]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-  };
-  auto step = [&](int t, const bf16x8 (&ac)[8], const bf16x8 (&bc)[4], bf16x8 (&an)[8], bf16x8 (&bn)[4]) {
-    if (t + 1 < nk) {
-      wait_next(t);
-      bar_raw();
-      if (t + 3 < nk) issue(t + 3);
-      read(t + 1, an, bn);
-    }
-    mma(ac, bc);
-  };
-
-  issue(0);
-  if (nk > 1) issue(1);
-  if (nk > 2) issue(2);
-  if (nk > 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bar_raw();
-  bf16x8 a0[8], b0[4], a1[8], b1[4];
-  read(0, a0, b0);
-  for (int t = 0; t < nk; t += 2) {
-    step(t, a0, b0, a1, b1);
-    if (t + 1 < nk) step(t + 1, a1, b1, a0, b0);
-  }
-  reg_epilogue<ACT, DROP, 8>(acc, e, C, ldc, M, N, m0 + wr * 128, n0 + wc * 64, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1888,16 +1261,14 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_grouped(GroupArgs ga) 
 
 // split-K plan for a plain-epilogue bf16 GEMM: only when the output has too few 128x128 tiles to
 // fill 256 CUs and K is long (the weight-gradient shapes). Returns 1 (no split) otherwise.
-int g_split_target = -1;  // blocks the split aims for (env MIT_SPLITK_TARGET; 128 beat 512 / 256 / 64 by 0.8-4 % in the step: fewer fp32 slabs)
-int g_split_target_dx = -1;  // the same for K-contig A (data gradients on the main stream; env MIT_SPLITK_TARGET_DX)
 int splitk_plan(long M, long N, long K, long* kchunk, int a_layout = MIT_MN_CONTIG) {
   const long tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   *kchunk = K;
-  if (g_split_target < 0) g_split_target = getenv("MIT_SPLITK_TARGET") ? atoi(getenv("MIT_SPLITK_TARGET")) : 128;
-  if (g_split_target_dx < 0)
-    g_split_target_dx = getenv("MIT_SPLITK_TARGET_DX") ? atoi(getenv("MIT_SPLITK_TARGET_DX")) : 256;  // 256 beat 128 by 0.4 % in the step (dX fc_out: K = 10000 on 128 tiles)
   if (tiles >= 256 || K < 1024 || N % 8) return 1;
-  const long target = a_layout == MIT_K_CONTIG ? g_split_target_dx : 256;  // 256 beat 128 by 0.4 % in the step (dX fc_out: K = 10000 on 128 tiles)
+  // blocks the split aims for: 256 for the data gradients (dX fc_out, K = 10000 on 128 tiles: +0.4 % step
+  // over 128) and the weight gradients (128 / 256 / 384 within +-0.3 % in the step)
+  const long target = 256;
+  (void)a_layout;
   long s = (target + tiles - 1) / tiles;
   s = min(s, K / 512);
   s = min(s, 16L);
@@ -1908,26 +1279,6 @@ int splitk_plan(long M, long N, long K, long* kchunk, int a_layout = MIT_MN_CONT
   return (int)((K + kc - 1) / kc);
 }
 long splitk_ws_bytes(long M, long N, int s) { return s > 1 ? 4096 + 4L * s * M * N + 4L * s * M : 0; }
-
-// split-K with the in-launch combine (any epilogue): grids of <= 128 output tiles -- the d_model =
-// 512 decoder GEMMs (M = B*T rows, N = 512: 128 tiles on 256 CUs) -- cut K so that about one block
-// runs per CU. Per-block latency, not throughput, bounds these.
-int fused_plan(long M, long N, long K, long* kchunk) {
-  const long tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  *kchunk = K;
-  if (tiles > 128 || N % 8) return 1;
-  long s = min(256 / tiles, K / 768);  // the combine costs ~4-5 us: only slices >= 12 K-tiles pay
-  s = min(s, 8L);
-  if (s < 2) return 1;
-  long kc = (K + s - 1) / s;
-  kc = (kc + BK - 1) / BK * BK;
-  *kchunk = kc;
-  return (int)((K + kc - 1) / kc);
-}
-long fused_ws_bytes(long M, long N, int s) {
-  const long tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  return s > 1 ? 4096 + 4L * s * tiles * BM * BN : 0;
-}
 
 // ------------------------------------------------------------------------------------------------
 // fp32 FMA kernel (parity mode): 64x64x16 tile, 256 threads x (4x4) outputs
@@ -2009,7 +1360,6 @@ constexpr long WS_HDR = 4096;
 struct Split {
   int ks = 1;
   long kchunk = 0;
-  bool fused = false;
 };
 
 int g_num_cus = 0;
@@ -2021,39 +1371,24 @@ int num_cus() {
   }
   return g_num_cus;
 }
-int g_w8 = -1;  // 8-wave 128 kernel: 0 = off, 1 = grids of <= one block per CU, 2 = always (env MIT_GEMM_W8)
-int waves8() {
-  if (g_w8 < 0) g_w8 = getenv("MIT_GEMM_W8") ? atoi(getenv("MIT_GEMM_W8")) : 2;
-  return g_w8;
-}
 
+// 8 waves per 128x128 block (2 per SIMD, each issuing half the LDS-DMA pieces of a K-tile): with 4
+// waves every K-tile's 8 DMA pieces per wave sat serially in front of its 32 MFMAs (+2.7 % step)
 template <int AL, int BL, int ACT, bool DROP>
 void launch_bf16(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, const Split& sp, hipStream_t s) {
   const int ksplit = sp.ks;
   const long kchunk = sp.ks > 1 ? sp.kchunk : g->K;
   float* ws = g->workspace ? (float*)((char*)g->workspace + WS_HDR) : nullptr;
-  int* cnt = sp.fused ? (int*)g->workspace : nullptr;
-  const long wsb = g->workspace ? max(0L, min(g->workspace_bytes - WS_HDR, (long)INT32_MAX)) : 0;
   const long nbm = (g->M + BM - 1) / BM, nbn = (g->N + BN - 1) / BN;
   const long nblk = nbm * nbn * ksplit;
   static bool attr = false;
   if (!attr) {
-    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 2>, smem_bytes(2));
-    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP, 2, 8>, smem_bytes(2));
+    set_lds(gemm_bf16_kernel<AL, BL, ACT, DROP>, smem_bytes(2));
     attr = true;
   }
-  // grids of at most one block per CU: 8 waves per block (2 per SIMD, each issuing half the LDS-DMA
-  // pieces of a K-tile) -- with one 4-wave block per CU every K-tile's 8 DMA pieces per wave sit
-  // serially in front of its 32 MFMAs
-  if (waves8() && (waves8() == 2 || nblk <= num_cus())) {
-    hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP, 2, 8>), dim3((unsigned)nblk), dim3(512), smem_bytes(2), s,
-                       (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                       b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
-    return;
-  }
-  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP, 2>), dim3((unsigned)nblk), dim3(256), smem_bytes(2), s,
+  hipLaunchKernelGGL((gemm_bf16_kernel<AL, BL, ACT, DROP>), dim3((unsigned)nblk), dim3(512), smem_bytes(2), s,
                      (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                     b_bytes, e, ksplit, kchunk, ws, g->rowsum, cnt, wsb);
+                     b_bytes, e, ksplit, kchunk, ws, g->rowsum);
 }
 
 template <int ACT, bool DROP>
@@ -2068,179 +1403,60 @@ void launch_rs(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, h
                      (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
 }
 
-int gemm_variant();
-int g_persist = -1;  // mit_gemm_set_persist; -1 = from env on first use
-// persistent 256 kernel (gemm256p_kernel): NT, gathered bf16 epilogue, more tiles than CUs, an even
-// K-tile count. Opt-in (MIT_G256_PERSIST=1; variant 8 forces the one-tile grid): alone it is 0-5 %
-// faster on the multi-round shapes (kv_all 93.1 -> 88.7 us, fc1+GELU 89.0 -> 86.9, CLIP-L o+res
-// 100.6 -> 103.9), but in the train step it is 9 % SLOWER (11605-11655 vs 12763-12806 pairs/s,
-// interleaved): a grid that holds every CU until its last tile starves the decoder's concurrent
-// kernels, which the one-tile grid lets in between tiles.
-template <int ACT, bool DROP>
-bool launch_256p(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
-  if (g_persist < 0) g_persist = getenv("MIT_G256_PERSIST") ? atoi(getenv("MIT_G256_PERSIST")) != 0 : 0;
-  const int on = g_persist;
-  const long tiles = ((g->M + 255) / 256) * ((g->N + B2 - 1) / B2), nk = (g->K + BK - 1) / BK;
-  const long G = (min((long)num_cus(), tiles) / 8) * 8;
-  if (!on || e.out_f32 || !epi_gatherable(e) || nk % 2 || G < 8 || tiles <= G) return false;
-  const bool ops = e.res || e.aux;
-  if (ops && ACT != MIT_ACT_NONE) return false;
-  static bool attr = false;
-  if (!attr) {
-    set_lds(gemm256p_kernel<ACT, DROP, 1>, SMEM2_BYTES);
-    if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256p_kernel<ACT, DROP, 2>, SMEM2_BYTES);
-    attr = true;
-  }
-  if constexpr (ACT == MIT_ACT_NONE) {
-    if (ops) {
-      hipLaunchKernelGGL((gemm256p_kernel<ACT, DROP, 2>), dim3((unsigned)G), dim3(512), SMEM2_BYTES, s,
-                         (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                         b_bytes, e);
-      return true;
-    }
-  }
-  hipLaunchKernelGGL((gemm256p_kernel<ACT, DROP, 1>), dim3((unsigned)G), dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
-                     (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
-  return true;
-}
+// 0 = pick per shape, 1 = always the 128x128 kernel, 2 = the 256x256 kernel wherever it has an
+// instance for the epilogue, 3 = the register-streaming kernel where it applies (tests / tools)
+int g_variant = 0;
+int gemm_variant() { return g_variant; }
 
-template <int AL, int BL, int ACT, bool DROP, int MI>
-void launch_256_mi(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
-  if constexpr (MI == 8 && AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
-    if (gemm_variant() != 8 && launch_256p<ACT, DROP>(g, e, a_bytes, b_bytes, s)) return;
-  }
-  const long nbm = (g->M + 32 * MI - 1) / (32 * MI), nbn = (g->N + B2 - 1) / B2;
+// bf16 outputs with a gatherable epilogue leave through each wave's LDS stage (STG 1: no operand,
+// STG 2: with the residual / aux block); f32 outputs and the other epilogues through registers
+template <int AL, int BL, int ACT, bool DROP>
+void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
+  const long nbm = (g->M + 255) / 256, nbn = (g->N + B2 - 1) / B2;
   static bool attr = false;
   if (!attr) {
-    set_lds(gemm256_kernel<AL, BL, ACT, DROP, MI>, SMEM2_BYTES);
-    if constexpr (MI == 8 && AL == MIT_K_CONTIG) {
-      set_lds(gemm256_kernel<AL, BL, ACT, DROP, MI, 1>, SMEM2_BYTES);
-      if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, MI, 2>, SMEM2_BYTES);
+    set_lds(gemm256_kernel<AL, BL, ACT, DROP>, SMEM2_BYTES);
+    if constexpr (AL == MIT_K_CONTIG) {
+      set_lds(gemm256_kernel<AL, BL, ACT, DROP, 1>, SMEM2_BYTES);
+      if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 2>, SMEM2_BYTES);
     }
     attr = true;
   }
-  if constexpr (MI == 8 && AL == MIT_K_CONTIG && MIT_G256_EPI_STAGE) {
-    // MIT_G256_STAGE: 0 = register epilogue everywhere, 1 = staged without operands only, 2 = staged
-    // everywhere it applies (default)
-    static const int on = getenv("MIT_G256_STAGE") ? atoi(getenv("MIT_G256_STAGE")) : 2;
+  const dim3 grid((unsigned)(nbm * nbn));
+  if constexpr (AL == MIT_K_CONTIG) {
     const bool ops = e.res || e.aux;
-    if (on && epi_gatherable(e) && !e.out_f32 && (!ops || on == 2)) {
+    if (epi_gatherable(e) && !e.out_f32) {
       if constexpr (ACT == MIT_ACT_NONE) {
         if (ops) {
-          hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, MI, 2>), dim3((unsigned)(nbm * nbn)), dim3(512),
-                             SMEM2_BYTES, s, (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda,
-                             g->ldb, g->ldc, a_bytes, b_bytes, e, 1, g->K, (float*)g->workspace, g->rowsum);
+          hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 2>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+                             (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
+                             (float*)g->workspace, g->rowsum);
           return;
         }
       }
       if (!ops) {
-        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, MI, 1>), dim3((unsigned)(nbm * nbn)), dim3(512),
-                           SMEM2_BYTES, s, (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb,
-                           g->ldc, a_bytes, b_bytes, e, 1, g->K, (float*)g->workspace, g->rowsum);
+        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 1>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+                           (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
+                           (float*)g->workspace, g->rowsum);
         return;
       }
     }
   }
-  hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, MI>), dim3((unsigned)(nbm * nbn)), dim3(512), SMEM2_BYTES, s,
-                     (const bf16*)g->A, (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes,
-                     b_bytes, e, 1, g->K, (float*)g->workspace, g->rowsum);
-}
-
-// 0 = pick per shape, 1 = always the 128x128 kernel, 2 = the 256x256 kernel wherever it has an
-// instance for the epilogue, 3 = the register-streaming kernel where it applies, 5 / 6 = the
-// 256-column kernel with 160 / 192-row tiles where it applies (tuning / tests)
-int g_variant = -1;
-
-// rows per wave of the 256-column kernel: 16 x (8, 6 or 5). Short tiles need K-contig A and the
-// register epilogue; among those the fewest (rounds of one tile per CU) x (per-tile time) wins, the
-// per-tile time modelled as a fixed part + K-steps at a per-row-count rate (tools/gemm_bench.py)
-int gemm_variant();
-int tile_mi(const mit_gemm_args* g, const Epi& e) {
-  static const int forced = getenv("MIT_G256_MI") ? atoi(getenv("MIT_G256_MI")) : 0;
-  const bool shortok = g->a_layout == MIT_K_CONTIG && epi_gatherable(e);
-  if (!shortok) return 8;
-  const int v = gemm_variant();
-  if (v == 5 || v == 6) return v;
-  if (forced == 5 || forced == 6) return forced;
-  // off by default: in the train step the encoder GEMMs run beside the decoder's kernels, and the
-  // 150-tile o-proj / fc2 grids leave 106 CUs to them -- 160-row tiles (237 blocks) measured 7 %
-  // slower end to end (11353-11414 vs 12205-12212 pairs/s interleaved) though 1-2 % faster alone.
-  // MIT_G256_MI=-1 enables the per-shape model below.
-  if (forced != -1) return 8;
-  const double cus = (double)num_cus(), nk = (double)((g->K + BK - 1) / BK), nbn = (double)((g->N + B2 - 1) / B2);
-  // per-tile K-step cost relative to MI = 8, measured on equal-round shapes (enc o / fc2, cfg3 o / fc2:
-  // 160-row tiles 0.98-0.99x the time of 256-row ones, 192-row 1.02-1.04x): the chip holds a lower
-  // clock when more CUs run MFMA loops, so shorter tiles pay only where they keep the round count
-  // (profiles/r02_gemm_short_tiles.txt)
-  const double FIX = 6.0, STEP = 1.54;  // us per tile, us per 64-deep K-step (MI = 8)
-  const int mis[3] = {8, 6, 5};
-  const double rate[3] = {1.0, 1.03, 0.975};
-  int best = 8;
-  double tbest = 1e30;
-  for (int i = 0; i < 3; ++i) {
-    const double tiles = (double)((g->M + 32 * mis[i] - 1) / (32 * mis[i])) * nbn;
-    const double t = std::ceil(tiles / cus) * (FIX + nk * STEP * rate[i]);
-    if (t < tbest * 0.995) {
-      tbest = t;
-      best = mis[i];
-    }
-  }
-  return best;
-}
-
-template <int ACT, bool DROP>
-void launch_tall(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    set_lds(gemm_tall_kernel<ACT, DROP>, T2_SMEM);
-    attr = true;
-  }
-  const long nb = ((g->M + 255) / 256) * ((g->N + 127) / 128);
-  hipLaunchKernelGGL((gemm_tall_kernel<ACT, DROP>), dim3((unsigned)nb), dim3(256), T2_SMEM, s, (const bf16*)g->A,
-                     (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
-}
-
-// the two-workgroup 256x128 kernel replaces the 256x256 one for NT GEMMs with a register
-// (gathered) epilogue: MIT_GEMM_TALL=0 keeps the 256x256 kernel; variant 7 forces it (tests)
-bool use_tall(const mit_gemm_args* g, const Epi& e) {
-  static int on = -1;
-  if (on < 0) on = getenv("MIT_GEMM_TALL") ? atoi(getenv("MIT_GEMM_TALL")) : 0;
-  if (g->a_layout != MIT_K_CONTIG || g->b_layout != MIT_K_CONTIG || !epi_gatherable(e)) return false;
-  const int v = gemm_variant();
-  return v == 7 || (v == 0 && on);
-}
-
-template <int AL, int BL, int ACT, bool DROP>
-void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, hipStream_t s) {
-  if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
-    if (use_tall(g, e)) return launch_tall<ACT, DROP>(g, e, a_bytes, b_bytes, s);
-  }
-  if constexpr (AL == MIT_K_CONTIG) {
-    switch (tile_mi(g, e)) {
-      case 6: return launch_256_mi<AL, BL, ACT, DROP, 6>(g, e, a_bytes, b_bytes, s);
-      case 5: return launch_256_mi<AL, BL, ACT, DROP, 5>(g, e, a_bytes, b_bytes, s);
-      default: break;
-    }
-  }
-  launch_256_mi<AL, BL, ACT, DROP, 8>(g, e, a_bytes, b_bytes, s);
-}
-int gemm_variant() {
-  if (g_variant < 0) g_variant = getenv("MIT_GEMM_VARIANT") ? atoi(getenv("MIT_GEMM_VARIANT")) : 0;
-  return g_variant;
+  hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+                     (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
+                     (float*)g->workspace, g->rowsum);
 }
 
 // register-streaming kernel (gemm_rs_kernel): the decode step's B-row GEMMs (M <= 256) with a short
 // K and N <= 2048 -- 7.2 vs 9.9 us per launch on 256 x {512, 1536, 2048} x 512. Everywhere else it
 // loses: each wave streams its own A and B fragments from L2 (8 FLOP per L2 byte vs 64 for the 128
 // kernel's LDS tiles): 2.5-3x slower on the M = 4032 decoder shapes, 2x on the decode fc_out
-// (tools/blas_reference.py, MIT_GEMM_RS=0 turns it off)
-int g_rs = -1;
+// (tools/blas_reference.py)
 bool use_rs(const mit_gemm_args* g) {
-  if (g_rs < 0) g_rs = getenv("MIT_GEMM_RS") ? atoi(getenv("MIT_GEMM_RS")) : 1;
   if (g->a_layout != MIT_K_CONTIG || g->b_layout != MIT_K_CONTIG || g->rowsum) return false;
   const int v = gemm_variant();
   if (v == 3) return true;
-  if (!g_rs || v != 0) return false;
+  if (v != 0) return false;
   return g->M <= 256 && g->N <= 2048 && g->K <= 1024;
 }
 
@@ -2250,7 +1466,7 @@ bool use_rs(const mit_gemm_args* g) {
 bool use_256(long M, long N, long K, int a_layout) {
   const int v = gemm_variant();
   if (v == 1) return false;
-  if (v == 2 || v == 5 || v == 6 || v == 7 || v == 8) return true;
+  if (v == 2) return true;
   // the MN-contig-A instances (weight gradients) exceed 256 VGPRs and spill: 128 kernel (+ split-K)
   if (a_layout != MIT_K_CONTIG) return false;
   if (M < 256 || N < 256 || K < 128) return false;
@@ -2325,8 +1541,6 @@ void launch_f32(const mit_gemm_args* g, const Epi& e, hipStream_t s) {
 
 inline bool al16(const void* p) { return ((uintptr_t)p % 16) == 0; }
 
-int g_fused = -1;  // in-launch split-K combine: -1 = from env on first use
-
 Split plan_split(const mit_gemm_args* g) {
   Split p;
   p.kchunk = g->K;
@@ -2341,54 +1555,21 @@ Split plan_split(const mit_gemm_args* g) {
       return p;
     }
   }
-  // off by default: in the train step the 128-block decoder GEMMs share the chip with the encoder
-  // prefetch and weight-gradient streams, and splitting them measured 0.6 % slower end to end
-  // (9645 vs 9700 pairs/s) though 8-18 % faster alone. MIT_GEMM_FUSED_SPLIT=1 or
-  // mit_gemm_set_fused_split(1) enables it.
-  if (g_fused < 0) g_fused = getenv("MIT_GEMM_FUSED_SPLIT") && atoi(getenv("MIT_GEMM_FUSED_SPLIT")) != 0;
-  // long-K data gradients only (K-contig A, K >= MIT_GEMM_FUSED_MINK; 0 = off): the decoder's
-  // linear1 / self in_proj dX (K = d_ff / 3 d on 128 tiles) run 24-32 K-steps per block. Measured
-  // -1.0 % (1536) / -0.3 % (2048) in the step (interleaved, 3 rounds): off
-  static long fused_mink = -1;
-  if (fused_mink < 0) fused_mink = getenv("MIT_GEMM_FUSED_MINK") ? atol(getenv("MIT_GEMM_FUSED_MINK")) : 0;
-  const bool fused = g_fused || (fused_mink > 0 && g->K >= fused_mink && g->a_layout == MIT_K_CONTIG);
-  if (fused && !g->rowsum && !use_256(g->M, g->N, g->K, g->a_layout)) {
-    const int s = fused_plan(g->M, g->N, g->K, &kc);
-    if (s > 1 && fused_ws_bytes(g->M, g->N, s) <= g->workspace_bytes) {
-      p.ks = s;
-      p.kchunk = kc;
-      p.fused = true;
-    }
-  }
   return p;
 }
 
 }  // namespace
 
 extern "C" int mit_gemm_set_variant(int v) {
-  MIT_CHECK_ARG((v >= 0 && v <= 3) || (v >= 5 && v <= 8), "mit_gemm_set_variant: %d not in {0,1,2,3,5,6,7,8}", v);
+  MIT_CHECK_ARG(v >= 0 && v <= 3, "mit_gemm_set_variant: %d not in {0,1,2,3}", v);
   g_variant = v;
-  return MIT_OK;
-}
-
-extern "C" int mit_gemm_set_persist(int on) {
-  MIT_CHECK_ARG(on == 0 || on == 1, "mit_gemm_set_persist: %d not in {0,1}", on);
-  g_persist = on;
-  return MIT_OK;
-}
-
-extern "C" int mit_gemm_set_fused_split(int on) {
-  MIT_CHECK_ARG(on == 0 || on == 1, "mit_gemm_set_fused_split: %d not in {0,1}", on);
-  g_fused = on;
   return MIT_OK;
 }
 
 extern "C" long mit_gemm_workspace_bytes(long M, long N, long K) {
   long kc;
-  const long a = max(splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc)),
-                     splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc, MIT_K_CONTIG)));
-  const long b = fused_ws_bytes(M, N, fused_plan(M, N, K, &kc));
-  return a > b ? a : b;
+  return max(splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc)),
+             splitk_ws_bytes(M, N, splitk_plan(M, N, K, &kc, MIT_K_CONTIG)));
 }
 
 extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
@@ -2460,7 +1641,7 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
     else if (g->a_layout == 0 && g->b_layout == 1) launch_layout<0, 1>(g, e, ab, bb, sp, big, s);
     else if (g->a_layout == 1 && g->b_layout == 0) launch_layout<1, 0>(g, e, ab, bb, sp, big, s);
     else launch_layout<1, 1>(g, e, ab, bb, sp, big, s);
-    if (sp.ks > 1 && !sp.fused) {
+    if (sp.ks > 1) {
       MIT_LAUNCH_CHECK("mit_gemm");
       const long total = g->M * (g->N / 4);
       long blocks = (total + 255) / 256;
@@ -2482,12 +1663,8 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
 // group split-K factor: about one block per CU over all problems -- at cfg1 (224 tiles per layer, 216
 // for the cross-K/V + projection pair) no split: 12482-12503 pairs/s vs 12278-12433 with 2 (two blocks
 // per CU), 12232-12263 with 3, 12081-12153 with 4 (interleaved, one box); the fp32 slabs and their
-// combine cost more than the shorter K loops save once the group fills the chip. Env
-// MIT_GROUPED_SPLIT overrides (A/B).
+// combine cost more than the shorter K loops save once the group fills the chip.
 long grouped_split(long tiles) {
-  static long forced = -1;
-  if (forced < 0) forced = getenv("MIT_GROUPED_SPLIT") ? atol(getenv("MIT_GROUPED_SPLIT")) : 0;
-  if (forced > 0) return min(forced, 16L);
   return tiles > 0 ? max(1L, min(16L, (long)num_cus() / tiles)) : 1;
 }
 
@@ -2538,8 +1715,7 @@ extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, const mit_ln_g
   const long s = grouped_split(tiles);
   GroupArgs ga;
   ga.n = n;
-  static const int grp = getenv("MIT_GROUPED_GROUP") ? atoi(getenv("MIT_GROUPED_GROUP")) : 1;
-  ga.group = grp > 0 ? grp : 1;
+  ga.group = 1;  // row-major tiles: an XCD's run of tiles shares the dY panel (FETCH 248 -> 225 MB)
   int start = 0, rstart = 0;
   bool any_split = false;
   char* wsp = (char*)workspace + WS_HDR;
@@ -2605,15 +1781,3 @@ extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, const mit_ln_g
   return MIT_OK;
 }
 
-#ifdef MIT_G256_STAMP
-// diagnostic build only: copy / clear the gemm256_kernel stamp buffer (tools/g256_stamps.py)
-extern "C" int mit_g256_stamps(unsigned long long* host, long n) {
-  const long cap = 16384L * G256_SLOTS;
-  if (n > cap) n = cap;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g256_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-extern "C" int mit_g256_stamps_clear() {
-  static unsigned long long zero[16384 * G256_SLOTS];
-  return hipMemcpyToSymbol(HIP_SYMBOL(g256_stamp), zero, sizeof(zero), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
-}
-#endif

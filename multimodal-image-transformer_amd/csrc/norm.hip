@@ -620,23 +620,17 @@ extern "C" int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x,
                    ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0;
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
-  static int wide = -1;  // env MIT_LN_WIDE=0: the 8-B-per-lane kernel for bf16 too (A/B)
-  if (wide < 0) wide = getenv("MIT_LN_WIDE") ? atoi(getenv("MIT_LN_WIDE")) : 1;
-  if (wide && dtype == MIT_BF16 && cols % 8 == 0 && cols <= 1024 && ldx % 8 == 0 && ldy % 8 == 0 &&
+  if (dtype == MIT_BF16 && cols % 8 == 0 && cols <= 1024 && ldx % 8 == 0 && ldy % 8 == 0 &&
       (!r || ldr % 8 == 0) && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)r | (uintptr_t)z) % 16) == 0 &&
       ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0) {
-    // RW rows per wave (env MIT_LN_RW = 1 / 2 / 4 for A/B). Alone (tools/ln_bench.py, interleaved):
-    // encoder 12608 x 768 9.4 / 10.2 / 11.6 us, CLIP-L 36928 x 1024 24.7 / 26.9 / 29.7 us, decoder
-    // 4032 x 512 + residual + dropout 6.3 / 6.5 / 8.7 us -- one row per wave: the most waves in flight
-    static const int rw_env = getenv("MIT_LN_RW") ? atoi(getenv("MIT_LN_RW")) : 0;
-    const int RWs = rw_env ? rw_env : 1;
-    // widths whose two rows fill whole 64-lane passes (256: 1 pass, 768: 3): two rows per wave
-    // (env MIT_LN_PAIR=0: the one-row form). Alone (tools/ln_bench.py, interleaved): 16384 x 256
+    // one row per wave (2 / 4 rows per wave alone, tools/ln_bench.py: encoder 12608 x 768 9.4 vs
+    // 10.2 / 11.6 us, CLIP-L 36928 x 1024 24.7 vs 26.9 / 29.7 us, decoder 4032 x 512 + residual +
+    // dropout 6.3 vs 6.5 / 8.7 us): the most waves in flight
+    // widths whose two rows fill whole 64-lane passes (256: 1 pass, 768: 3): two rows per wave. Alone (tools/ln_bench.py, interleaved): 16384 x 256
     // 6.1 vs 7.6-8.2 us, 12608 x 768 + residual + dropout (configs[3]'s decoder width) 18.3 vs
     // 19.7-20.0 us; the encoder's 768-wide LayerNorm without residual is not faster (10.0 vs 9.9 us:
     // x -> y alone copies in 6.2 us, the rest is per-row latency) and keeps the one-row form
-    static const int pair = getenv("MIT_LN_PAIR") ? atoi(getenv("MIT_LN_PAIR")) : 1;
-    if (pair && !rw_env && (cols == 256 || (cols == 768 && r))) {
+    if ((cols == 256 || (cols == 768 && r))) {
       const dim3 g2((unsigned)((rows + 7) / 8));
       auto go = [&](auto nvc) {
         constexpr int NVc = decltype(nvc)::value;
@@ -666,11 +660,7 @@ extern "C" int mit_layernorm_fwd(int dtype, long rows, long cols, const void* x,
                            (const bf16*)r, ldr, seed, site, th, sc, dropout, gamma, beta, eps, (bf16*)z, (bf16*)y, ldy,
                            mean, rstd);
     };
-    auto by_rw = [&](auto nvc) {
-      if (RWs == 1) launch(nvc, std::integral_constant<int, 1>());
-      else if (RWs == 2) launch(nvc, std::integral_constant<int, 2>());
-      else launch(nvc, std::integral_constant<int, 4>());
-    };
+    auto by_rw = [&](auto nvc) { launch(nvc, std::integral_constant<int, 1>()); };
     if (cols <= 512) by_rw(std::integral_constant<int, 1>());
     else by_rw(std::integral_constant<int, 2>());
     MIT_LAUNCH_CHECK("mit_layernorm_fwd");
@@ -805,9 +795,7 @@ extern "C" int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy
                          (const T*)z, mean, rstd, gamma, (T*)dx, (T*)dr, seed, site, th, sc, dropout, ws);
     });
   };
-  static int wide = -1;  // env MIT_LN_WIDE=0: the 8-B-per-lane kernels for bf16 too (A/B)
-  if (wide < 0) wide = getenv("MIT_LN_WIDE") ? atoi(getenv("MIT_LN_WIDE")) : 1;
-  if (wide && dtype == MIT_BF16 && cols % 8 == 0 && cols <= 1024 &&
+  if (dtype == MIT_BF16 && cols % 8 == 0 && cols <= 1024 &&
       (((uintptr_t)dy | (uintptr_t)z | (uintptr_t)dx | (uintptr_t)dr | (uintptr_t)gamma) % 16) == 0) {
     if (cols <= 512)
       hipLaunchKernelGGL((ln_bwd_wide_kernel<1>), dim3((unsigned)nblk), dim3(256), 0, s, rows, cols, (const bf16*)dy,

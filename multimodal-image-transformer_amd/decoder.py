@@ -329,17 +329,15 @@ class TransformerDecoder:
         self.pe = sinusoidal_pe(max_seq_len, embed_dim).to(self.device)
         self.training = True
         self._acts: Dict[tuple, _Acts] = {}
-        # weight-gradient GEMMs on a second stream (MIT_DW_SIDE_STREAM=0 disables, for A/B)
-        self.dw_side_stream = os.environ.get("MIT_DW_SIDE_STREAM", "1") != "0"
-        # a decoder layer's six weight gradients as ONE grouped launch (native.gemm_grouped) on the side
-        # stream, bf16 only (MIT_DW_GROUPED=0: one GEMM each, as they become ready)
-        self.dw_grouped = os.environ.get("MIT_DW_GROUPED", "1") != "0"
-        # the cross-K/V weight gradient (all layers' dY final once layer 0's cross-attention backward
-        # ran) goes out on the side stream right then, ahead of layer 0's grouped dW, instead of with
-        # the projection's after the memory gradient at the end of the backward
-        self.kv_dw_early = os.environ.get("MIT_KV_DW_EARLY", "1") != "0"
+        # weight-gradient GEMMs on a second stream; in bf16 a decoder layer's six weight gradients go out
+        # as ONE grouped launch (native.gemm_grouped; fp32 parity mode: one GEMM each, as they become
+        # ready); the cross-K/V weight gradient (all layers' dY final once layer 0's cross-attention
+        # backward ran) goes out right then, ahead of layer 0's grouped dW
+        self.dw_side_stream = True
+        self.dw_grouped = True
+        self.kv_dw_early = True
         self._side = None
-        self.side_priority = 0  # set by ImageToTextModel.train_step (high priority beside the encoder)
+        self.side_priority = 0
         if self._own_store:
             self.init_weights(0)
 

@@ -31,29 +31,6 @@ from decoder import TransformerDecoder, decoder_entries, flat_to_reference, refe
 from encoder import VisionEncoder, build_encoder
 from params import FlatParams
 
-# MIT_PROFILE_REUSE_ENCODER=1 (what-if profiling, never for results): prefetch_encoder reuses the
-# previous encoder output for the same image tensor instead of recomputing it
-_PROFILE_REUSE_ENCODER = os.environ.get("MIT_PROFILE_REUSE_ENCODER") == "1"
-_STREAM_PRIORITY = os.environ.get("MIT_STREAM_PRIORITY", "0") == "1"  # measured neutral: opt-in
-# Prefetched encoder spread over the step: layers [0, MIT_ENC_SPLIT) start with the step, the rest
-# once the decoder forward is enqueued and done ("fwd") or after the backward ("bwd"); default: the
-# whole encoder at the start of the step (MIT_ENC_SPLIT unset). Measured neutral (split 6 / 9 after
-# the forward: +0.3 / +0.2 %, 11 after the backward: -1.1 %, tools/gpu_ab.sh -k prefetch): the step is
-# bound by the CU-time of its kernels, not by where the encoder's launches sit in it
-_ENC_SPLIT = int(os.environ.get("MIT_ENC_SPLIT", "-1"))
-_ENC_GATE = os.environ.get("MIT_ENC_GATE", "fwd")
-# The prefetch that overwrites an arena slot waits only for the end of the backward of the step that
-# read it (a per-slot event), not for everything on the main stream: the encoder then runs beside
-# that step's clip + AdamW (HBM-bound) instead of after them. MIT_ENC_SLOT_EVENT=0: the old wait.
-_ENC_SLOT_EVENT = os.environ.get("MIT_ENC_SLOT_EVENT", "1") != "0"
-
-
-def _high_priority() -> int:
-    """The highest stream priority the runtime offers (torch: lower number = higher priority)."""
-    lo, hi = torch.cuda.Stream.priority_range()
-    return min(lo, hi)
-
-
 def _dtype_from_config(dtype):
     if dtype is None:
         dtype = config.DTYPE
@@ -157,11 +134,8 @@ class ImageToTextModel:
         self._enc_stream = None
         self._enc_slot = 0
         self._prefetched = None
-        self._last_pf = None
-        self._pf_rest = None
         self._slot_free = None           # native.HipEvents(2): end of the backward of the step that read slot i
         self._slot_freed = [False, False]  # slot i's event recorded since the slot was last read
-        self._hi_stream = None
         self._params: Optional["OrderedDict[str, torch.nn.Parameter]"] = None
         self._gen = 0  # bumped by every forward that writes the shared arenas (autograd staleness check)
 
@@ -226,39 +200,11 @@ class ImageToTextModel:
         enc = self.encoder.forward(images, rows="all", slot=slot)  # [B, N, E]
         return enc.reshape(B * N, E), E, N
 
-    def _encoder_rows_split(self, images: torch.Tensor, slot: int, split: int):
-        """_encoder_rows in two launch segments: layers [0, split) now, rest() -> (rows, ld, S)."""
-        B = images.shape[0]
-        N, E = self.encoder.N, self.encoder.E
-        cls = self.memory_mode == "cls"
-        rest = self.encoder.forward_split(images, rows="cls" if cls else "all", slot=slot, split=split)
-
-        def finish():
-            enc = rest()
-            return (enc, N * E, 1) if cls else (enc.reshape(B * N, E), E, N)
-        return finish
-
-    def _continue_prefetch(self):
-        """Launch the deferred encoder layers on the prefetch stream, after the main stream's work so far."""
-        if self._pf_rest is None:
-            return
-        rest, self._pf_rest = self._pf_rest, None
-        enc = self._enc_stream.cuda_stream
-        self._enc_events.wait_stream(enc, native.stream_ptr())
-        with torch.cuda.stream(self._enc_stream):
-            out = rest()
-        ev = self._enc_events.record(enc)
-        images, slot = self._prefetched[:2]
-        self._prefetched = self._last_pf = (images, slot, out, ev)
-
     def prefetch_encoder(self, images: torch.Tensor):
         """Start the frozen encoder's forward for the NEXT batch on a second stream; the next
         train_step(images) consumes it instead of recomputing. The encoder has no trainable state, so
         its output does not depend on the step in between: the result is identical, and its GEMMs
         fill the CUs the decoder's small kernels leave idle. Double-buffered arenas (slot 0/1)."""
-        if _PROFILE_REUSE_ENCODER and self._last_pf is not None and self._last_pf[0].data_ptr() == images.data_ptr():
-            self._prefetched = self._last_pf  # what-if profiling only: step time without the encoder
-            return
         if self._enc_stream is None:
             self._enc_stream = torch.cuda.Stream(device=self.device)
             self._enc_events = native.HipEvents(8)
@@ -266,21 +212,17 @@ class ImageToTextModel:
         images = images.to(self.device, non_blocking=True)
         enc = self._enc_stream.cuda_stream
         # the arena's previous reader (two steps back) is done: the encoder stream waits for the end of
-        # that step's backward (its last read: the projection weight gradient), or for main
-        if _ENC_SLOT_EVENT and self._slot_freed[slot]:
+        # that step's backward (its last read: the projection weight gradient; the encoder then runs
+        # beside that step's HBM-bound clip + AdamW: +0.2 %), or for everything on main (the autograd
+        # path records no slot event)
+        if self._slot_freed[slot]:
             native.HipEvents.wait(enc, self._slot_free.pool[slot])
         else:
             self._enc_events.wait_stream(enc, native.stream_ptr())
-        self._continue_prefetch()  # an earlier prefetch's deferred layers (not consumed by a step)
-        if 0 < _ENC_SPLIT < self.encoder.L:
-            with torch.cuda.stream(self._enc_stream):
-                self._pf_rest = self._encoder_rows_split(images, slot, _ENC_SPLIT)
-            self._prefetched = (images, slot, None, None)
-            return
         with torch.cuda.stream(self._enc_stream):
             out = self._encoder_rows(images, slot)
         ev = self._enc_events.record(enc)
-        self._prefetched = self._last_pf = (images, slot, out, ev)
+        self._prefetched = (images, slot, out, ev)
 
     def _encode_memory(self, images: torch.Tensor, refresh: bool = True):
         """Returns (mem_rows, mem_ld, S, enc_rows, enc_ld): memory [B*S rows of d] and the
@@ -290,7 +232,6 @@ class ImageToTextModel:
         E, d = self.encoder.E, self.decoder_embed_dim
         self.store.ensure_shadow(force=refresh)
         self._gen += 1
-        self._continue_prefetch()
         pf, self._prefetched = self._prefetched, None
         if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
             _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
@@ -387,21 +328,9 @@ class ImageToTextModel:
     # --- fused train step (train.py:75-93) -----------------------------------------------------
     def train_step(self, images: torch.Tensor, decoder_input_tokens: torch.Tensor, target_tokens: torch.Tensor,
                    dist=None, next_images: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """See _train_step. The step's own kernels (main + weight-gradient streams) are issued on
-        HIGH-priority streams, the frozen encoder's one-step-ahead prefetch on a normal one: the
-        command processors then dispatch the step's chain first and the encoder's large GEMMs fill
-        the CUs it leaves idle. Opt-in (MIT_STREAM_PRIORITY=1): measured neutral (10271 vs 10311 pairs/s)."""
-        if not _STREAM_PRIORITY or torch.cuda.is_current_stream_capturing():
-            return self._train_step(images, decoder_input_tokens, target_tokens, dist, next_images)
-        if self._hi_stream is None:
-            self._hi_stream = torch.cuda.Stream(device=self.device, priority=_high_priority())
-            self.decoder.side_priority = _high_priority()
-        caller = torch.cuda.current_stream(self.device)
-        self._hi_stream.wait_stream(caller)
-        with torch.cuda.stream(self._hi_stream):
-            loss = self._train_step(images, decoder_input_tokens, target_tokens, dist, next_images)
-        caller.wait_stream(self._hi_stream)
-        return loss
+        """See _train_step. (Stream priorities for the step's own streams over the encoder prefetch
+        measured neutral to -1.7 %, DESIGN.md §4.1c: all streams run at the default priority.)"""
+        return self._train_step(images, decoder_input_tokens, target_tokens, dist, next_images)
 
     def _train_step(self, images: torch.Tensor, decoder_input_tokens: torch.Tensor, target_tokens: torch.Tensor,
                     dist=None, next_images: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -420,8 +349,6 @@ class ImageToTextModel:
         A = dec.acts(B, T, S, True)
         native.step_inc(self.seed_t)
         logits, _ = dec.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, True)
-        if _ENC_GATE == "fwd":
-            self._continue_prefetch()
         native.zero(A.count)
         native.zero(A.loss_sum)
         native.count_targets(targets, self.decoder_pad_idx, A.count)
@@ -438,8 +365,6 @@ class ImageToTextModel:
             self._slot_free.record_at(self._enc_slot, native.stream_ptr())
             self._slot_freed[self._enc_slot] = True
         native.scalar_div(A.loss_sum, A.count, A.loss)
-        if _ENC_GATE == "bwd":
-            self._continue_prefetch()
         if dist is not None:
             dist.finish_backward(A.loss)
         return A.loss

@@ -18,6 +18,7 @@ from torch.utils._python_dispatch import TorchDispatchMode
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MIT_HIP_LIB", os.path.join(_HERE, "lib", "libmit_hip.so"))
+ABI_VERSION = 3  # mit_abi_version() of the library this binding matches (include/mit_hip.h)
 
 F32, BF16 = 0, 1
 K_CONTIG, MN_CONTIG = 0, 1
@@ -78,8 +79,6 @@ SIGNATURES = {
     "mit_gemm_workspace_bytes": (L, [L, L, L]),
     "mit_gemm_set_variant": (I, [I]),
     "mit_gemm_plan": (I, [ctypes.POINTER(GemmArgs), ctypes.POINTER(I)]),
-    "mit_gemm_set_fused_split": (I, [I]),
-    "mit_gemm_set_persist": (I, [I]),
     "mit_gemm_grouped_ws_bytes": (L, [ctypes.POINTER(GemmArgs), I]),
     "mit_gemm_grouped": (I, [ctypes.POINTER(GemmArgs), I, ctypes.POINTER(LnGradsJob), I, vp, L, vp]),
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
@@ -142,6 +141,8 @@ def load_library(path: str = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.mit_abi_version() != ABI_VERSION:
+        raise NativeError(f"{path}: ABI version {lib.mit_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 
@@ -328,7 +329,7 @@ class _NoTorchKernels(TorchDispatchMode):
                "t", "transpose", "permute", "unsqueeze", "squeeze", "expand", "split", "split_with_sizes",
                "chunk", "unbind", "flatten", "contiguous", "empty", "empty_like", "empty_strided", "view_as",
                "_reshape_alias", "lift_fresh", "sym_size", "sym_stride", "sym_numel", "sym_storage_offset",
-               "is_same_size", "_local_scalar_dense", "item", "_to_copy", "to", "record_stream", "set_"}
+               "is_same_size", "_local_scalar_dense", "item", "record_stream", "set_"}
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
@@ -337,7 +338,10 @@ class _NoTorchKernels(TorchDispatchMode):
             def on_gpu(x):
                 return isinstance(x, torch.Tensor) and x.is_cuda
             flat = list(args) + list(kwargs.values())
-            if any(on_gpu(x) or (isinstance(x, (list, tuple)) and any(on_gpu(y) for y in x)) for x in flat):
+            # a copy / cast ONTO the GPU (host-to-device, e.g. CPU or int32 tokens in train_step) enqueues
+            # a copy kernel too: the replay would read the recording run's temporary
+            to_gpu = name == "_to_copy" and torch.device(kwargs.get("device") or "cpu").type == "cuda"
+            if to_gpu or any(on_gpu(x) or (isinstance(x, (list, tuple)) and any(on_gpu(y) for y in x)) for x in flat):
                 raise NativeError(f"native.record: torch op {func} would enqueue GPU work while recording; a "
                                   f"replay re-issues only native launches and would drop it (do it outside the "
                                   f"recorded function, or through a native entry point / host_call)")
@@ -486,19 +490,8 @@ def set_gemm_probe(probe):
 
 def gemm_set_variant(v):
     """0 = per-shape tile-kernel choice, 1 = 128x128 only, 2 = 256x256 wherever legal, 3 = 64x64
-    register-streaming kernel for NT GEMMs, 5 / 6 = the 256-column kernel with 160 / 192-row tiles
-    wherever legal (K-contig A, gatherable epilogue; else its 256-row tile)."""
+    register-streaming kernel for NT GEMMs."""
     _check(lib().mit_gemm_set_variant(int(v)), "mit_gemm_set_variant")
-
-
-def gemm_set_fused_split(on):
-    """In-launch split-K combine for the <= 128-tile GEMMs (off by default)."""
-    _check(lib().mit_gemm_set_fused_split(1 if on else 0), "mit_gemm_set_fused_split")
-
-
-def gemm_set_persist(on):
-    """Persistent 256x256 kernel for multi-round NT GEMMs (off by default: slower in the train step)."""
-    _check(lib().mit_gemm_set_persist(1 if on else 0), "mit_gemm_set_persist")
 
 
 def gemm_plan(g):

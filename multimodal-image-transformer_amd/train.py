@@ -348,6 +348,13 @@ def main(argv=None):
         tl = train_one_epoch(model, train, opt, None, "cuda", config.GRAD_CLIP_VALUE, sched, epoch,
                              config.LOG_INTERVAL if rank == 0 else 0, None, dist=dp)
         vl = evaluate(model, val, None, "cuda")
+        if world > 1:
+            # every rank takes rank 0's validation loss, so the best-checkpoint decision (and the barrier
+            # around the save) is the same on all ranks even if their losses differ in the last ulp
+            on = "cuda" if tdist.get_backend() == "nccl" else "cpu"
+            t = torch.tensor([vl], dtype=torch.float64, device=on)
+            tdist.broadcast(t, 0)
+            vl = t.item()
         history.append((tl, vl))
         if rank == 0:
             print(f"epoch {epoch + 1}: train {tl:.4f} val {vl:.4f} ({time.time() - t0:.1f}s, {world} rank(s))", flush=True)
@@ -355,8 +362,8 @@ def main(argv=None):
             best = vl
             if rank == 0:
                 print("saved", save_checkpoint(model, opt, epoch, vl, args.out, sched))
-            if world > 1:
-                tdist.barrier()
+        if world > 1:
+            tdist.barrier()
     return history
 
 

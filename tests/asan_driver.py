@@ -16,8 +16,7 @@ import native  # noqa: E402
 SAFE_ZERO = {  # entry points that are valid with all-zero / null arguments or only query
     "mit_last_error", "mit_abi_version", "mit_gemm_workspace_bytes", "mit_gemm_grouped_ws_bytes",
     "mit_layernorm_bwd_ws_floats", "mit_colsum_ws_floats", "mit_grad_norm_ws_floats", "mit_plan_begin",
-    "mit_plan_end", "mit_plan_size", "mit_plan_destroy", "mit_gemm_set_variant", "mit_gemm_set_fused_split",
-    "mit_gemm_set_persist",
+    "mit_plan_end", "mit_plan_size", "mit_plan_destroy", "mit_gemm_set_variant",
     "mit_gemm_plan", "mit_embed_plan_ints", "mit_event_record", "mit_stream_wait_event"}
 
 

@@ -21,8 +21,6 @@ def _lib():
     N.load_library()
     yield
     N.gemm_set_variant(0)
-    N.gemm_set_fused_split(0)
-    N.gemm_set_persist(0)
 
 
 def _ops(M, Nn, K, al, bl, seed=0):
@@ -128,47 +126,6 @@ def test_gemm_gelu_epilogue_accuracy():
         assert err < 2e-5 * ref.abs().max().item(), (v, err)
 
 
-@pytest.mark.parametrize("al,bl", [(0, 0), (0, 1)])
-@pytest.mark.parametrize("M,Nn,K", [(4032, 512, 1536), (4032, 512, 2048), (1000, 520, 3072), (200, 136, 4096)])
-@pytest.mark.parametrize("epi", ["plain", "bias_res", "relu_drop", "aux_f32acc", "gelu"])
-def test_gemm_split_k_in_launch_combine(al, bl, M, Nn, K, epi):
-    """Split-K with the in-launch combine (<= 128 output tiles, any epilogue): equal to the same
-    GEMM without a workspace (no split) up to fp32 summation order, bit-identical over repeats
-    (the combine sums slabs in slice order whatever the arrival order), counters left at zero."""
-    N.gemm_set_fused_split(1)
-    A, B, ref = _ops(M, Nn, K, al, bl, seed=M + K)
-    g = torch.Generator().manual_seed(3)
-    kw = {}
-    out_dt = torch.bfloat16
-    if epi == "bias_res":
-        kw = dict(bias=torch.randn(Nn, generator=g).to(dev()), residual=torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16))
-    elif epi == "relu_drop":
-        kw = dict(act=N.ACT_RELU, drop_p=0.25, seed=torch.tensor([11], device=dev()), site=3)
-    elif epi == "aux_f32acc":
-        kw = dict(aux=torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16), aux_scale=1.5, accumulate=True)
-        out_dt = torch.float32
-    elif epi == "gelu":
-        kw = dict(act=N.ACT_GELU, bias=torch.randn(Nn, generator=g).to(dev()))
-    ws = N.gemm_workspace(M, Nn, K, dev())
-    args = N.GemmArgs(N.BF16, al, bl, M, Nn, K, A.data_ptr(), K if al == 0 else M, B.data_ptr(),
-                      K if bl == 0 else Nn, 0, Nn, 1.0, None, 0, None, Nn, None, Nn, 1.0, 0.0, None, 0, 0, 0, None,
-                      ws.data_ptr(), ws.numel() * 4)
-    tile, ks = N.gemm_plan(args)
-    assert tile == 128 and ks >= 2, (tile, ks)
-    base = torch.randn(M, Nn, generator=g).to(dev(), out_dt)
-    outs = []
-    for w in (None, ws, ws, ws):
-        C = base.clone()
-        N.gemm(A, B, C, M, Nn, K, a_layout=al, b_layout=bl, workspace=w, **kw)
-        outs.append(C)
-    assert torch.equal(outs[1], outs[2]) and torch.equal(outs[1], outs[3])
-    assert torch.count_nonzero(ws[:1024]).item() == 0
-    d = (outs[1].float() - outs[0].float()).abs().max().item()
-    scale = max(outs[0].float().abs().max().item(), 1.0)
-    assert d <= (2e-2 if out_dt == torch.bfloat16 else 1e-4) * scale, d
-
-
-
 @pytest.mark.parametrize("M,Nn,K", [(4032, 512, 512), (4032, 512, 2048), (256, 10000, 512), (250, 520, 200),
                                     (1000, 136, 1096), (64, 64, 64), (70, 2048, 72)])
 def test_register_streaming_kernel(M, Nn, K):
@@ -204,102 +161,3 @@ def test_register_streaming_kernel(M, Nn, K):
     C2 = torch.empty_like(C)
     N.gemm(A, B, C2, M, Nn, K)
     assert torch.equal(C, C2), "register-streaming kernel not deterministic"
-
-
-@pytest.mark.parametrize("M,Nn,K", [(200, 264, 72), (961, 776, 200), (1000, 768, 3072), (12608, 768, 768)])
-@pytest.mark.parametrize("epi", ["plain", "bias_res", "gelu", "f32"])
-def test_gemm256_short_tiles_bit_identical(M, Nn, K, epi):
-    """160 / 192-row tiles (variants 5 / 6) run the same per-element MFMA K order as the 256-row tile,
-    so every epilogue's output is bit-identical, ragged M included."""
-    g = torch.Generator().manual_seed(3)
-    x = torch.randn(M, K, generator=g).to(dev(), torch.bfloat16)
-    w = (torch.randn(Nn, K, generator=g) / 10).to(dev(), torch.bfloat16)
-    kw = {}
-    if epi == "bias_res":
-        kw = dict(bias=torch.randn(Nn, generator=g).to(dev()), residual=torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16))
-    elif epi == "gelu":
-        kw = dict(bias=torch.randn(Nn, generator=g).to(dev()), act=N.ACT_GELU)
-    outs = {}
-    for v in (2, 6, 5):
-        N.gemm_set_variant(v)
-        C = torch.full((M, Nn), float("nan"), device=dev(), dtype=torch.float32 if epi == "f32" else torch.bfloat16)
-        N.gemm(x, w, C, M, Nn, K, **kw)
-        outs[v] = C
-    ref = x.float() @ w.float().t()
-    if epi == "plain" or epi == "f32":
-        assert _rel(outs[2], ref) < 8e-3
-    for v in (6, 5):
-        assert torch.equal(outs[v], outs[2]), f"variant {v}"
-
-
-TALL_SHAPES = [(256, 128, 32), (264, 136, 72), (520, 776, 200), (1000, 520, 136), (2056, 768, 1536), (12608, 2304, 768)]
-
-
-@pytest.mark.parametrize("M,Nn,K", TALL_SHAPES)
-def test_gemm_tall_bit_identical_to_256(M, Nn, K):
-    """The two-workgroup 256x128 kernel (gemm_tall_kernel, variant 7) runs every output element's MFMAs
-    in the same K order as the 256x256 kernel (32-deep chunks in sequence), so NT outputs are
-    bit-identical; and within the fp32 reference's tolerance."""
-    A, B, ref = _ops(M, Nn, K, 0, 0, seed=4)
-    g = torch.Generator().manual_seed(6)
-    bias = torch.randn(Nn, generator=g).to(dev())
-    res = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
-    seed = torch.tensor([5], dtype=torch.int64, device=dev())
-    cases = [dict(f32=True), dict(bias=bias), dict(bias=bias, act=N.ACT_GELU), dict(residual=res),
-             dict(bias=bias, act=N.ACT_RELU, drop_p=0.1, seed=seed, site=3), dict(bias=bias, act=N.ACT_QUICK_GELU)]
-    for kw in cases:
-        f32 = kw.pop("f32", False)
-        outs = []
-        for v in (7, 2):
-            N.gemm_set_variant(v)
-            C = torch.empty(M, Nn, device=dev(), dtype=torch.float32 if f32 else torch.bfloat16)
-            N.gemm(A, B, C, M, Nn, K, **kw)
-            outs.append(C)
-        assert torch.equal(outs[0], outs[1]), (kw.keys(), (outs[0].float() - outs[1].float()).abs().max().item())
-        if f32:
-            assert _rel(outs[0], ref) < 1e-5
-
-
-def test_gemm_tall_race_screen():
-    N.gemm_set_variant(7)
-    M, Nn, K = 4104, 2312, 776
-    A, B, ref = _ops(M, Nn, K, 0, 0, seed=7)
-    C0 = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
-    N.gemm(A, B, C0, M, Nn, K)
-    assert _rel(C0, ref) < 8e-3
-    C = torch.empty_like(C0)
-    bad = 0
-    for _ in range(30):
-        C.fill_(0)
-        N.gemm(A, B, C, M, Nn, K)
-        bad += int(not torch.equal(C, C0))
-    assert bad == 0, f"{bad}/30 repeats differ bitwise (LDS race)"
-
-
-@pytest.mark.parametrize("M,Nn,K", [(4104, 4104, 768), (4352, 4096, 200), (12608, 2304, 768)])
-def test_gemm256_persistent_bit_identical(M, Nn, K):
-    """Multi-round NT grids run on the persistent 256 kernel (gemm256p_kernel: the next tile's first
-    K-tile loaded during this tile's two-pass staged epilogue); variant 8 forces the one-tile grid.
-    Same K loop and epilogue arithmetic: outputs bit-identical for every epilogue, and repeatable."""
-    A, B, ref = _ops(M, Nn, K, 0, 0, seed=8)
-    g = torch.Generator().manual_seed(9)
-    bias = torch.randn(Nn, generator=g).to(dev())
-    res = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
-    seed = torch.tensor([11], dtype=torch.int64, device=dev())
-    cases = [dict(), dict(bias=bias), dict(bias=bias, act=N.ACT_GELU), dict(residual=res, bias=bias),
-             dict(bias=bias, act=N.ACT_RELU, drop_p=0.1, seed=seed, site=3)]
-    N.gemm_set_persist(1)
-    for kw in cases:
-        outs = []
-        for v in (0, 8, 0):
-            N.gemm_set_variant(v)
-            C = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
-            N.gemm(A, B, C, M, Nn, K, **kw)
-            outs.append(C)
-        assert torch.equal(outs[0], outs[1]), (list(kw), (outs[0].float() - outs[1].float()).abs().max().item())
-        assert torch.equal(outs[0], outs[2])
-    N.gemm_set_persist(0)
-    N.gemm_set_variant(0)
-    C = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
-    N.gemm(A, B, C, M, Nn, K)
-    assert _rel(C, ref) < 8e-3

@@ -250,16 +250,11 @@ def test_graphed_step_matches_eager():
     torch.testing.assert_close(p1, p0, rtol=0, atol=1e-4)
 
 
-@pytest.mark.parametrize("split,gate", [(-1, "fwd"), (1, "fwd"), (1, "bwd")])
-def test_encoder_prefetch_matches_inline(split, gate, monkeypatch):
+def test_encoder_prefetch_matches_inline():
     """train_step(..., next_images=...) runs the frozen encoder of the next batch one step ahead on
     a second stream (double-buffered arenas); losses and parameters equal the inline schedule,
-    including when the batch changes between steps -- also with the prefetch in two launch segments
-    (MIT_ENC_SPLIT / MIT_ENC_GATE: layer 1 of 2 deferred to after the forward / the backward)."""
-    import model as MD
+    including when the batch changes between steps."""
     import optim
-    monkeypatch.setattr(MD, "_ENC_SPLIT", split)
-    monkeypatch.setattr(MD, "_ENC_GATE", gate)
     meta, T = FX.load("tiny_vit_patches")
     batches = [[t.cuda() for t in FX.inputs(meta, s)] for s in range(3)]
     res = []

@@ -45,3 +45,26 @@ def test_replayed_steps_equal_eager_steps(dtype):
     assert s0 == s1 == 8
     assert l0 == l1, (l0, l1)
     assert torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("kind", ["cpu", "int32"])
+def test_record_rejects_token_copies(kind):
+    """A step fed CPU or int32 tokens converts them with a device copy / cast kernel inside train_step;
+    a replay would not repeat it (it would read the recording run's temporary), so native.record
+    raises instead of recording a silently wrong plan."""
+    import native
+    import optim
+    meta, _ = FX.load("tiny_vit_patches")
+    imgs, di, tg = [t.cuda() for t in FX.inputs(meta, 0)]
+    m, _ = build_model(meta, torch.bfloat16, dropout=0.0)
+    m.train()
+    opt = optim.AdamW(m.parameters(), lr=1e-3)
+    di_bad = di.cpu() if kind == "cpu" else di.to(torch.int32)
+
+    def step():
+        m.train_step(imgs, di_bad, tg)
+        opt.step(5.0)
+    step()
+    with pytest.raises(native.NativeError, match="would enqueue GPU work"):
+        native.record(step)
+    torch.cuda.synchronize()

@@ -7,11 +7,9 @@
 # rounds: of bench.py (--no-cpu-baseline --no-roofline; prints "variant round value ms_per_step"), or
 # with -m of a kernel micro-benchmark (tools/gemm_bench.py, attn_bench.py, ln_bench.py; a variant
 # "ARGS=..." passes its arguments, e.g. ARGS=2,6,5 for gemm_bench's tile variants). Variants may
-# select a library build with MIT_HIP_LIB=<path> (e.g. attention.hip built with -DMIT_ATTN_LAZY=8).
-# The numbers in DESIGN §4.1c / §4.1d / §5.1 were taken this way, e.g. MIT_DW_GROUPED, MIT_GROUPED_SPLIT,
-# MIT_STREAM_PRIORITY, MIT_SPLITK_TARGET(_DX), MIT_GEMM_FUSED_MINK, MIT_G256_MI, MIT_ATTN_PAD,
-# MIT_LN_RW / MIT_LN_WIDE, MIT_ENC_SPLIT / MIT_ENC_GATE, MIT_KV_DW_EARLY, and for -w decode
-# MIT_DECODE_FUSED, MIT_DECODE_LONGK, MIT_DECODE_ROWS_ATTN, MIT_DECODE_STREAMS, MIT_DECODE_LAUNCH.
+# select a library build with MIT_HIP_LIB=<path> (tools/build_variants.sh builds one with compile-time
+# flags); that is how kernel variants are compared (the round-1..3 run-time knobs of DESIGN §4.1c /
+# §4.1d / §5.1 were measured this way and have since been folded into their measured defaults).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 W=train; R=2; K=; MB=
 while getopts "k:m:w:r:" o; do

@@ -38,6 +38,40 @@ def pmc(db, counter):
     return {short(r[0]): {"launches": int(r[1]), "avg_kib": float(r[2]), "avg_ns": float(r[3])} for r in rows}
 
 
+def sq_pass(db):
+    """Per kernel (template head + its full name's template arguments folded in by short()): averages of the
+    MFMA-busy pass (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE) and the
+    quantities derived from them (MI355X_MICROARCH.md):
+      eff_clock_ghz   = GRBM_GUI_ACTIVE / 8 XCDs / dispatch wall time (reads high below ~0.3 ms dispatches)
+      mfma_busy_frac  = SQ_VALU_MFMA_BUSY_CYCLES (summed over the 1024 SIMDs) / (1024 x GRBM_GUI_ACTIVE / 8),
+                        the share of SIMD-cycles of the dispatch in which the MFMA pipe was busy"""
+    c = sqlite3.connect(db)
+    rows = c.execute("select kernel_name, counter_name, count(*), avg(value), avg(duration) from counters_collection "
+                     "group by kernel_name, counter_name").fetchall()
+    out = {}
+    for name, ctr, n, v, dur in rows:
+        e = out.setdefault(inst(name), {"launches": int(n), "avg_ns": float(dur)})
+        e[ctr] = float(v)
+    for k, e in out.items():
+        g = e.get("GRBM_GUI_ACTIVE")
+        if g:
+            cyc = g / 8.0
+            e["eff_clock_ghz"] = round(cyc / e["avg_ns"], 3)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in e:
+                e["mfma_busy_frac"] = round(e["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc), 4)
+            if "SQ_BUSY_CYCLES" in e:
+                e["sq_busy_frac"] = round(e["SQ_BUSY_CYCLES"] / (8.0 * cyc), 4)
+    return out
+
+
+def inst(name: str) -> str:
+    """short() plus the first template arguments, so the instances of one kernel stay apart."""
+    n = name.replace("(anonymous namespace)::", "")
+    n = re.sub(r"^void ", "", n)
+    m = re.match(r"^([\w:]+<[^()]*?>)", n)
+    return m.group(1) if m else short(name)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace", required=True)
@@ -45,6 +79,8 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--command", default="")
+    ap.add_argument("--sq", default=None, help="rocpd database of the MFMA-busy pass (SQ_VALU_MFMA_BUSY_CYCLES "
+                    "SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE)")
     ap.add_argument("--trace-csv", default=None, help="kernel trace CSV of the same run: the GEMM launches of "
                     "bench.py's roofline replay (after the last AdamW) averaged per (kernel, a_layout, b_layout)")
     ap.add_argument("--bench-json", default=None, help="bench.py output line to cross-check")
@@ -98,6 +134,13 @@ def main():
         if f_ is not None and w_ is not None:
             e["hbm_bytes_per_launch"] = round((2 * f_["avg_kib"] + w_["avg_kib"]) * 1024)
         out["kernels"][k] = e
+    if a.sq:
+        sq = sq_pass(a.sq)
+        out["mfma_pass"] = {
+            "counters": "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE (one pass of their own)",
+            "derived": "eff_clock_ghz = GRBM_GUI_ACTIVE/8/wall; mfma_busy_frac = MFMA_BUSY/(1024 SIMDs x GRBM_GUI_ACTIVE/8)",
+            "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in e.items()}
+                        for k, e in sorted(sq.items(), key=lambda kv: -kv[1]["avg_ns"] * kv[1]["launches"])[:40]}}
     with open(a.out + "_pmc.json", "w") as f:
         json.dump(out, f, indent=1)
     for s, _, n, tot, avg, pct in ks[:12]:
