@@ -299,6 +299,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const long b = blockIdx.z, h = blockIdx.y;
   const long qblk = (long)blockIdx.x * AQ;
+  MIT_DASSERT(h < H && qblk < Lq && Lk > 0);
   const long qi = qblk + w * 16 + (lane & 15);
   const bool qlive = qi < Lq;
   const bf16* Kb = (const bf16*)a.k + b * a.k_batch + h * D;
@@ -511,6 +512,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
   char* Vs = lds + (long)lkp * 128;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, nw = blockDim.x >> 6;
   const long h = blockIdx.x, b = blockIdx.y;
+  MIT_DASSERT(h < H && Lk <= lkp && lkp <= HK_MAX && Lq > 0);
   const bf16* Kb = (const bf16*)a.k + b * a.k_batch + h * D;
   const bf16* Vb = (const bf16*)a.v + b * a.v_batch + h * D;
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, kbytes, 0x00020000);
@@ -1002,6 +1004,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
   float* Dl = Ls + 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const long h = blockIdx.x, b = blockIdx.y, bh = b * H + h;
+  MIT_DASSERT(h < H && Lq <= 64 && Lk <= lkp && lkp <= HB_MAXK);
   const bf16* Qb = (const bf16*)a.q + b * a.q_batch + h * D;
   const bf16* Kb = (const bf16*)a.k + b * a.k_batch + h * D;
   const bf16* Vb = (const bf16*)a.v + b * a.v_batch + h * D;

@@ -110,41 +110,42 @@ __device__ __forceinline__ float gelu_fast(float x) {
 }
 
 // gelu_fast on two values with packed FP32 math (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of
-// the polynomial per instruction); the rcp / exp stay scalar. Same operations, same results.
+// the polynomial per instruction); the rcp / exp stay scalar. The A&S 7.1.26 evaluation with the
+// constants folded: t = 1 / (1 + (0.3275911/sqrt2)|x|), h = Phi(-|x|) = t * (P(t)/2) * 2^(-x^2 log2(e)/2)
+// (the 0.5 in the coefficients, the exp's log2(e)/2 in one multiply of x^2), y = x >= 0 ? x - x h : x h
+// (enc fc1+GELU 85.3-88.1 vs 88.9-90.3 us with the unfolded form, step +0.25 %).
 typedef __attribute__((ext_vector_type(2))) float f32x2;
-#ifndef MIT_GELU2_V2  // the reassociated form below (A/B switch; enc fc1+GELU 85.3-88.1 vs 88.9-90.3 us
-#define MIT_GELU2_V2 1  // alone, step +0.25 %, interleaved on one box)
-#endif
 __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
-  if (MIT_GELU2_V2) {
-    // the same A&S 7.1.26 evaluation with the constants folded: t = 1 / (1 + (0.3275911/sqrt2)|x|),
-    // h = Phi(-|x|) = t * (P(t)/2) * 2^(-x^2 log2(e)/2) (the 0.5 in the coefficients, the exp's
-    // log2(e)/2 in one multiply of x^2), y = x >= 0 ? x - x h : x h
-    const f32x2 ax = __builtin_elementwise_abs(x);
-    const f32x2 d = __builtin_elementwise_fma(f32x2{0.23164189f, 0.23164189f}, ax, f32x2{1.0f, 1.0f});
-    const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
-    f32x2 p = __builtin_elementwise_fma(f32x2{0.5307027145f, 0.5307027145f}, t, f32x2{-0.7265760135f, -0.7265760135f});
-    p = __builtin_elementwise_fma(p, t, f32x2{0.7107068705f, 0.7107068705f});
-    p = __builtin_elementwise_fma(p, t, f32x2{-0.142248368f, -0.142248368f});
-    p = __builtin_elementwise_fma(p, t, f32x2{0.127414796f, 0.127414796f});
-    const f32x2 z = (x * x) * -0.72134752044448170f;  // -x^2/2 in log2 units
-    const f32x2 e = {__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])};
-    const f32x2 xh = x * (p * t * e);
-    const f32x2 xm = x - xh;
-    return f32x2{x[0] >= 0.0f ? xm[0] : xh[0], x[1] >= 0.0f ? xm[1] : xh[1]};
-  }
-  const f32x2 a = __builtin_elementwise_abs(x) * 0.70710678118654752f;
-  const f32x2 d = __builtin_elementwise_fma(f32x2{0.3275911f, 0.3275911f}, a, f32x2{1.0f, 1.0f});
+  const f32x2 ax = __builtin_elementwise_abs(x);
+  const f32x2 d = __builtin_elementwise_fma(f32x2{0.23164189f, 0.23164189f}, ax, f32x2{1.0f, 1.0f});
   const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
-  f32x2 p = __builtin_elementwise_fma(f32x2{1.061405429f, 1.061405429f}, t, f32x2{-1.453152027f, -1.453152027f});
-  p = __builtin_elementwise_fma(p, t, f32x2{1.421413741f, 1.421413741f});
-  p = __builtin_elementwise_fma(p, t, f32x2{-0.284496736f, -0.284496736f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.254829592f, 0.254829592f});
-  const f32x2 na2 = -a * a;
-  const f32x2 e = {__expf(na2[0]), __expf(na2[1])};
-  const f32x2 h = 0.5f * p * t * e;
-  return x * f32x2{x[0] >= 0.0f ? 1.0f - h[0] : h[0], x[1] >= 0.0f ? 1.0f - h[1] : h[1]};
+  f32x2 p = __builtin_elementwise_fma(f32x2{0.5307027145f, 0.5307027145f}, t, f32x2{-0.7265760135f, -0.7265760135f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.7107068705f, 0.7107068705f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.142248368f, -0.142248368f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.127414796f, 0.127414796f});
+  const f32x2 z = (x * x) * -0.72134752044448170f;  // -x^2/2 in log2 units
+  const f32x2 e = {__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])};
+  const f32x2 xh = x * (p * t * e);
+  const f32x2 xm = x - xh;
+  return f32x2{x[0] >= 0.0f ? xm[0] : xh[0], x[1] >= 0.0f ? xm[1] : xh[1]};
 }
+
+// Kernel extent asserts (sanitizers): compiled in only by the diagnostic build
+// (`make -C multimodal-image-transformer_amd/csrc asserts` -> lib/variants/libmit_hip_asserts.so, loaded with
+// MIT_LIB=...; tests/test_asserts_gpu.py runs GEMMs and attentions under it). A failing assert traps the
+// kernel with the file:line of the violated extent instead of reading or writing out of range. The
+// shipped library compiles none of it.
+#ifndef MIT_DEVICE_ASSERTS
+#define MIT_DEVICE_ASSERTS 0
+#endif
+#if MIT_DEVICE_ASSERTS
+#include <cassert>
+#define MIT_DASSERT(cond) assert(cond)
+#else
+#define MIT_DASSERT(cond) \
+  do {                    \
+  } while (0)
+#endif
 
 // error plumbing shared by every C-ABI entry point (capi.cpp)
 int mit_set_error(const char* fmt, ...);

@@ -27,7 +27,8 @@
 //     evaluated behind runtime flags costs ~20 % of a K=768 GEMM); bias / residual / aux-mask /
 //     f32-accumulate stay runtime flags.
 //   * tile order: XCD-aware remap + row grouping so tiles sharing A/B panels share an L2.
-// fp32 path (parity mode): a plain LDS-tiled FMA kernel with the identical epilogue semantics.
+// fp32 path (parity mode): an LDS-tiled kernel on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32) with the
+// identical epilogue semantics.
 #include <stdlib.h>
 
 #include <cmath>
@@ -372,6 +373,8 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
   const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
   const int bn = (bid % (GROUP * nbn)) / gsize;
   const long m0 = (long)bm * BM, n0 = (long)bn * BN;
+  MIT_DASSERT(blk < nwg && split < ksplit && bm < nbm && bn < nbn && m0 < M && n0 < N);
+  MIT_DASSERT(lda >= (ALAY == MIT_K_CONTIG ? K : M) && ldb >= (BLAY == MIT_K_CONTIG ? K : N) && ldc >= N);
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
@@ -866,6 +869,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
   const int bn = (bid % (GROUP * nbn)) / gsize;
   const long m0 = (long)bm * BMT, n0 = (long)bn * B2;
+  MIT_DASSERT((int)blockIdx.x < ntiles && bm < nbm && bn < nbn && m0 < M && n0 < N);
+  MIT_DASSERT(lda >= (ALAY == MIT_K_CONTIG ? K : M) && ldb >= (BLAY == MIT_K_CONTIG ? K : N) && ldc >= N);
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
@@ -1112,6 +1117,7 @@ __global__ __launch_bounds__(256) void gemm_rs_kernel(const bf16* __restrict__ A
   const int bid = xcd_remap(blockIdx.x, nbm * nbn);  // an XCD's blocks: consecutive row blocks share A
   const int bm = bid / nbn, bn = bid % nbn;
   const long m0 = (long)bm * 64, n0 = (long)bn * 64;
+  MIT_DASSERT((int)blockIdx.x < nbm * nbn && m0 < M && n0 < N && lda >= K && ldb >= K && ldc >= N);
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
 
@@ -1281,21 +1287,31 @@ int splitk_plan(long M, long N, long K, long* kchunk, int a_layout = MIT_MN_CONT
 long splitk_ws_bytes(long M, long N, int s) { return s > 1 ? 4096 + 4L * s * M * N + 4L * s * M : 0; }
 
 // ------------------------------------------------------------------------------------------------
-// fp32 FMA kernel (parity mode): 64x64x16 tile, 256 threads x (4x4) outputs
+// fp32 kernel (parity mode) on the exact-f32 matrix cores: v_mfma_f32_32x32x2_f32 (f32 in, f32
+// accumulate; each MFMA is a chain of correctly rounded f32 FMAs, MI355X_MICROARCH.md: 155 TF vs the
+// VALU's 52 on a GEMM). 64x64x16 block tile, 4 waves (2 x 2) of 32x32, A / B staged k-major in LDS
+// (both operand layouts, any edges: out-of-range elements stage as 0), 8 MFMAs per wave per K-tile.
+// Same run-time epilogue (epi_store) and fused row sums as the bf16 kernels.
+// MFMA 32x32x2 operand layout: lane l gives A(m = l & 31, k = l >> 5) and B(k = l >> 5, n = l & 31);
+// accumulator j of lane l is C(8 (j >> 2) + 4 (l >> 5) + (j & 3), l & 31).
 // ------------------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(16))) float f32x16;
 template <int ALAY, int BLAY>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ A, const float* __restrict__ B, void* C,
                                                        long M, long N, long K, long lda, long ldb, long ldc, Epi e,
                                                        float* __restrict__ rowsum) {
-  __shared__ float As[16][64 + 4];
-  __shared__ float Bs[16][64 + 4];
-  const int tid = threadIdx.x;
-  const long m0 = (long)blockIdx.y * 64, n0 = (long)blockIdx.x * 64;
-  const int tm = (tid >> 4) * 4, tn = (tid & 15) * 4;
-  float acc[4][4] = {};
-  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
-  const bool do_rs = rowsum != nullptr && blockIdx.x == 0 && tn == 0;
-  for (long k0 = 0; k0 < K; k0 += 16) {
+  constexpr int FT = 64, FK = 16, FP = FT + 4;
+  __shared__ float As[FK][FP];
+  __shared__ float Bs[FK][FP];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const long m0 = (long)blockIdx.y * FT, n0 = (long)blockIdx.x * FT;
+  MIT_DASSERT(m0 < M && n0 < N && ldc >= N);
+  f32x16 acc = {};
+  float rsum = 0.f;
+  const bool do_rs = rowsum != nullptr && blockIdx.x == 0 && wn == 0;
+  const int lm = lane & 31, lk = lane >> 5;
+  for (long k0 = 0; k0 < K; k0 += FK) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int id = tid + 256 * i;  // 0..1023 over 64 x 16
@@ -1314,34 +1330,22 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     }
     __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      float a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[kk][tm + i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tn + j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
-      if (do_rs) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rsum[i] += a[i];
-      }
+    for (int kk = 0; kk < FK; kk += 2) {
+      const float a = As[kk + lk][wm * 32 + lm], b = Bs[kk + lk][wn * 32 + lm];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      if (do_rs) rsum += a;
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long r = m0 + tm + i, c = n0 + tn + j;
-      if (r < M && c < N) epi_store<float>(e, C, ldc, N, r, c, acc[i][j]);
-    }
-  if (do_rs) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (m0 + tm + i < M) rowsum[m0 + tm + i] = rsum[i];
+  for (int j = 0; j < 16; ++j) {
+    const long r = m0 + wm * 32 + 8 * (j >> 2) + 4 * lk + (j & 3), c = n0 + wn * 32 + lm;
+    if (r < M && c < N) epi_store<float>(e, C, ldc, N, r, c, acc[j]);
+  }
+  if (do_rs) {  // lanes l and l + 32 hold the even / odd k of row l & 31
+    rsum += __shfl_xor(rsum, 32, 64);
+    const long r = m0 + wm * 32 + lm;
+    if (lane < 32 && r < M) rowsum[r] = rsum;
   }
 }
 

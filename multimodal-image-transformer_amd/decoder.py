@@ -786,6 +786,50 @@ class TransformerDecoder:
         native.greedy_pick_advance(stt.logits, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished,
                                    stt.n_finished, stt.ticket, V=V)
 
+    def forward_ops(self, tokens: torch.Tensor, mem: torch.Tensor, S: int, params: Dict[str, torch.Tensor],
+                    seed: Optional[torch.Tensor], drop_p: float, mem_keys: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The forward of run_forward built from torch.ops.mit_hip operators (ops.py), so torch's autograd
+        records it and ``loss.backward()`` runs each op's HIP backward (the reference loop, train.py:80-100).
+        tokens int64 [B, T]; mem [B*S, d] memory rows (may require grad: the projection's output);
+        params: the trainable f32 tensors by flat entry name (the model's nn.Parameters), whose compute-dtype
+        shadows (store.w) the GEMMs read. Returns f32 logits [B, T, V]. Same kernels, dropout sites and
+        seeds as run_forward: the same values."""
+        import ops
+        mh = ops.load()
+        B, T = tokens.shape
+        d, H, L = self.d, self.H, self.L
+        st = self.store
+        lp = (lambda n: st.w(n)) if st.shadow is not st.master else (lambda n: None)  # noqa: E731
+        P = params
+        sc = 1.0 / math.sqrt(self.hd)
+        x = mh.embedding(tokens, P["token_embedding.weight"], self.pe, math.sqrt(d), drop_p, seed, EMB_SITE,
+                         lp("token_embedding.weight"), self.pad_idx)
+        kv = mh.linear(mem, P["cross_kv.weight"], P["cross_kv.bias"], weight_lp=lp("cross_kv.weight")).view(B, S, L * 2 * d)
+        for l in range(L):
+            q = f"layers.{l}."
+            base = 64 * l
+
+            def lin(t, n):
+                return mh.linear(t, P[q + n + ".weight"], P[q + n + ".bias"], weight_lp=lp(q + n + ".weight"))
+
+            def ln(t, r, k, site):
+                return mh.layer_norm_train(t, P[q + f"norm{k}.weight"], P[q + f"norm{k}.bias"], 1e-5, r, drop_p, seed,
+                                           site)[0]
+            qkv = lin(x, "self_in")
+            o = mh.attention_train(qkv[..., :d], qkv[..., d:2 * d], qkv[..., 2 * d:], H, True, sc, tokens,
+                                   self.pad_idx, drop_p, seed, base + 0)[0]
+            x1 = ln(x, lin(o, "self_out"), 1, base + 1)
+            kvl = kv[..., l * 2 * d:(l + 1) * 2 * d]
+            oc = mh.attention_train(lin(x1, "cross_q"), kvl[..., :d], kvl[..., d:], H, False, sc, mem_keys, 0, drop_p,
+                                    seed, base + 2)[0]
+            x2 = ln(x1, lin(oc, "cross_out"), 2, base + 3)
+            y = mh.ffn(x2, P[q + "linear1.weight"], P[q + "linear1.bias"], P[q + "linear2.weight"],
+                       P[q + "linear2.bias"], drop_p, seed, base + 4, lp(q + "linear1.weight"),
+                       lp(q + "linear2.weight"))[0]
+            x = ln(x2, y, 3, base + 5)
+        logits = mh.linear(x, P["fc_out.weight"], P["fc_out.bias"], out_f32=True, weight_lp=lp("fc_out.weight"))
+        return logits if self.Vp == self.V else logits[..., :self.V]
+
     def forward(self, tgt_tokens: torch.Tensor, memory: torch.Tensor, memory_padding_mask=None) -> torch.Tensor:
         """decoder.py:134-193: f32 logits [B, T, V] (no autograd; training goes through the model's
         train step). memory_padding_mask: bool [B, S], True = padded memory position, masked out of

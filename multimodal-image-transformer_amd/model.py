@@ -60,29 +60,6 @@ class GraphedStep:
         return self.loss
 
 
-class _ModelFunction(torch.autograd.Function):
-    """``logits = model(images, tokens)`` with autograd, for the reference loop shape
-    (train.py:80-100: criterion(logits) -> loss.backward() -> clip_grad_norm_(model.parameters())
-    -> optimizer.step()). forward runs the HIP forward keeping every layer's activations in the
-    training arena; backward runs the HIP backward (decoder.run_backward) and hands the gradients
-    to the parameters as views of the flat gradient buffer. ``anchor`` is one trainable parameter:
-    it makes autograd record the node; no gradient flows through it (the gradients are attached to
-    every parameter directly)."""
-
-    @staticmethod
-    def forward(ctx, anchor, model, images, tokens):
-        out, state = model._forward_for_autograd(images, tokens)
-        ctx.model, ctx.state = model, state
-        return out
-
-    @staticmethod
-    @torch.autograd.function.once_differentiable
-    def backward(ctx, dlogits):
-        ctx.model._backward_for_autograd(dlogits, ctx.state)
-        ctx.state = None
-        return None, None, None, None
-
-
 class ImageToTextModel:
     def __init__(self, decoder_vocab_size: int, decoder_embed_dim: int, decoder_heads: int, decoder_layers: int,
                  decoder_ff_dim: int, decoder_max_seq_len: int, decoder_dropout: float, decoder_pad_idx: int, *,
@@ -160,9 +137,23 @@ class ImageToTextModel:
         if self._params is None:
             self._params = OrderedDict((n, torch.nn.Parameter(self.store.p(n), requires_grad=True))
                                        for n in self.store.names())
-            for p in self._params.values():
+            for n, p in self._params.items():
                 p._mit_store = self.store  # optim.AdamW(model.parameters()) finds the flat buffers
+                p.register_post_accumulate_grad_hook(self._grad_to_flat(n))
         return self._params
+
+    def _grad_to_flat(self, name):
+        """After autograd accumulated a parameter's gradient (model(images, tokens) -> loss.backward()):
+        make p.grad the view of the flat gradient buffer (one copy when autograd created a new tensor),
+        so clip_grad_norm_, torch.optim.AdamW, the fused optim.AdamW and the DP buckets all see it."""
+        st = self.store
+
+        def hook(p):
+            g = st.g(name)
+            if p.grad is not None and p.grad.data_ptr() != g.data_ptr():
+                g.copy_(p.grad)
+                p.grad = g
+        return hook
 
     def parameters(self, recurse: bool = True) -> Iterator[torch.nn.Parameter]:
         """The trainable parameters (projection + decoder; the encoder is frozen, model.py:87-90)
@@ -255,8 +246,7 @@ class ImageToTextModel:
         autograd node whose backward runs the HIP backward (the reference's loss.backward(),
         train.py:93); otherwise a forward-only launch sequence."""
         if torch.is_grad_enabled() and any(p.requires_grad for p in self._param_table().values()):
-            anchor = next(iter(self._param_table().values()))
-            return _ModelFunction.apply(anchor, self, image_tensors, tgt_tokens)
+            return self._forward_ops(image_tensors, tgt_tokens)
         images = image_tensors.to(self.device)
         tokens = tgt_tokens.to(self.device, torch.int64).contiguous()
         B, T = tokens.shape
@@ -271,59 +261,40 @@ class ImageToTextModel:
 
     __call__ = forward
 
-    def _forward_for_autograd(self, image_tensors, tgt_tokens):
+    def _forward_ops(self, image_tensors, tgt_tokens):
+        """model(images, tokens) under autograd (the reference loop, train.py:80-100): the frozen encoder
+        runs as usual (no gradient), the projection and the decoder as torch.ops.mit_hip operators
+        (ops.py, decoder.forward_ops) whose registered backward formulas run the HIP backward kernels.
+        Parameter gradients land in the flat gradient buffer (see _param_table's hooks)."""
+        import ops
+        mh = ops.load()
         images = image_tensors.to(self.device)
         tokens = tgt_tokens.to(self.device, torch.int64).contiguous()
         B, T = tokens.shape
-        mem, mem_ld, S, enc_rows, enc_ld = self._encode_memory(images)
-        dec = self.decoder
-        A = dec.acts(B, T, S, True)
-        p = dec.dropout if self.training else 0.0
+        self.store.ensure_shadow(force=True)
+        self._gen += 1
+        pf, self._prefetched = self._prefetched, None
+        if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
+            _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
+            native.HipEvents.wait(native.stream_ptr(), ev)
+        else:
+            enc_rows, enc_ld, S = self._encoder_rows(images, self._enc_slot)
+        E = self.encoder_output_dim
+        # the encoder arena is reused by the next forward: the projection's saved input is a copy
+        enc = torch.as_strided(enc_rows, (B * S, E), (enc_ld, 1)).clone()
+        P = self._param_table()
+        p = self.decoder.dropout if self.training else 0.0
+        seed = None
         if p > 0:
             native.step_inc(self.seed_t)
-        out = torch.empty(B * T, dec.Vp, dtype=torch.float32, device=self.device)
-        dec.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, True, logits_out=out, drop_p=p)
-        proj = (enc_rows, enc_ld, self.encoder_output_dim) if self.has_projection else None
-        return dec.unpad_logits(out, B, T), (self._gen, tokens, mem, mem_ld, S, A, proj)
-
-    def _backward_for_autograd(self, dlogits: torch.Tensor, state):
-        gen, tokens, mem, mem_ld, S, A, proj = state
-        if gen != self._gen:
-            raise RuntimeError("ImageToTextModel: backward() after a later forward — the model keeps ONE step's "
-                               "activations (HBM arenas reused every step); call backward before the next forward")
-        dec, st = self.decoder, self.store
-        R, V, Vp = tokens.numel(), dec.V, dec.Vp
-        dl = A.logits  # compute-dtype [R, Vp] gradient of the head output; pad columns exactly 0
-        g = dlogits.reshape(R, V)
-        if Vp == V and dl.dtype != torch.float32:
-            native.cast_f32(g.contiguous(), dl)
+            seed = self.seed_t.clone()  # the backward regenerates this forward's masks whatever runs between
+        if self.has_projection:
+            st = self.store
+            mem = mh.linear(enc, P["projection.weight"], P["projection.bias"],
+                            weight_lp=st.w("projection.weight") if st.shadow is not st.master else None)
         else:
-            if Vp != V:
-                dl[:, V:].zero_()
-            dl[:, :V].copy_(g)
-        params = self._param_table()
-        # autograd accumulates into existing .grad: keep the previous values of the parameters whose
-        # .grad already is our view (zero_grad(set_to_none=False) or a second backward)
-        views = {n: p.grad is not None and p.grad.data_ptr() == st.g(n).data_ptr() for n, p in params.items()}
-        prev = None
-        if any(views.values()):
-            prev = st.grad.clone()
-            for n, is_view in views.items():
-                if not is_view:
-                    _, off, cnt = st.index[n]
-                    prev[off:off + cnt].zero_()
-        # the dropout masks are regenerated from the seed the forward used (seed_t is unchanged:
-        # no forward ran in between, checked above)
-        dec.run_backward(tokens, mem, mem_ld, S, A, self.seed_t, dl, proj_input=proj)
-        if prev is not None:
-            st.grad.add_(prev)
-        for n, p in params.items():
-            if not p.requires_grad or views[n]:
-                continue
-            if p.grad is None:
-                p.grad = st.g(n)
-            else:
-                p.grad.add_(st.g(n))
+            mem = enc
+        return self.decoder.forward_ops(tokens, mem, S, P, seed, p)
 
     # --- fused train step (train.py:75-93) -----------------------------------------------------
     def train_step(self, images: torch.Tensor, decoder_input_tokens: torch.Tensor, target_tokens: torch.Tensor,

@@ -68,6 +68,10 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
     if dist is not None and not fused:
         raise ValueError("data-parallel training runs the fused step: pass optim.AdamW and the reference criterion")
     total = torch.zeros(1, dtype=torch.float32, device=model.device)
+    # failure detection: the index of the first batch whose loss is NaN / inf, tracked on the
+    # device (no per-step sync; the reference's all-PAD rows give NaN, dataset.py:116-130), checked at every
+    # log point and at the end of the epoch
+    first_bad = torch.full((1,), -1, dtype=torch.int64, device=model.device)
     n = 0
     it = _staged(model, dataloader)
     batch = next(it, None)
@@ -85,7 +89,11 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
             optimizer.zero_grad()
             logits = model(batch["images"], batch["decoder_input_tokens"])
             tgt = batch["target_tokens"].to(model.device)
-            loss = criterion(logits.view(-1, logits.size(-1)), tgt.reshape(-1))
+            if _fused_loss_ok(model, criterion):  # the reference criterion: the CE row kernel (mit_hip::cross_entropy)
+                import ops
+                loss = ops.load().cross_entropy(logits, tgt.to(torch.int64), model.decoder_pad_idx)[0]
+            else:
+                loss = criterion(logits.view(-1, logits.size(-1)), tgt.reshape(-1))
             loss.backward()
             if grad_clip_value > 0:
                 torch.nn.utils.clip_grad_norm_(model.parameters(), grad_clip_value)
@@ -94,15 +102,30 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
         if scheduler:
             scheduler.step()
         total += loss
+        bad = ~torch.isfinite(loss)
+        first_bad.copy_(torch.where(bad & (first_bad < 0), torch.full_like(first_bad, i), first_bad))
         n += 1
         if log_interval and (i + 1) % log_interval == 0:
+            _raise_if_bad(first_bad, epoch)
             lv = loss.item()
             print(f"epoch {epoch + 1} batch {i + 1}: loss {lv:.4f} lr {_lr_of(optimizer):.2e}", flush=True)
             if wandb_run:
                 wandb_run.log({"train_batch_loss": lv, "learning_rate": _lr_of(optimizer),
                                "global_step": epoch * max(1, len(dataloader)) + i + 1})
         batch = nxt
+    _raise_if_bad(first_bad, epoch)
     return (total / max(n, 1)).item()
+
+
+class NonFiniteLossError(FloatingPointError):
+    """A training batch produced a NaN / inf loss (e.g. a batch whose targets are all PAD)."""
+
+
+def _raise_if_bad(first_bad: torch.Tensor, epoch: int):
+    i = int(first_bad.item())
+    if i >= 0:
+        raise NonFiniteLossError(f"epoch {epoch + 1}: non-finite training loss at batch {i + 1} (step index {i}); "
+                                 f"the parameters were updated with it -- check the batch (all-PAD targets give NaN)")
 
 
 @torch.no_grad()

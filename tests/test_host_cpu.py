@@ -159,3 +159,34 @@ def test_optimizer_state_maps_torch_adamw_format(name):
     with pytest.raises(optim.OptimizerStateError):
         opt.load_state_dict({"step": 1, "exp_avg": before})
     assert torch.equal(store.exp_avg, before)
+
+
+def test_train_one_epoch_raises_on_non_finite_loss():
+    """Failure detection: a NaN loss (the reference's all-PAD batch) stops the epoch with
+    the step index instead of training on; the check runs on the device flag at log points / epoch end."""
+    import torch
+    import train as TR
+
+    class Tiny(torch.nn.Module):
+        device = torch.device("cpu")
+        decoder_pad_idx = 0
+
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Linear(4, 5)
+
+        def forward(self, images, tokens):
+            return self.w(images.flatten(1)).unsqueeze(1).expand(-1, tokens.shape[1], -1).contiguous()
+
+    m = Tiny()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+
+    def crit(logits, tgt):  # the all-PAD batch: 0 / 0
+        keep = tgt != 0
+        return torch.nn.functional.cross_entropy(logits[keep], tgt[keep], reduction="sum") / keep.sum()
+    batches = [{"images": torch.randn(2, 4), "decoder_input_tokens": torch.ones(2, 3, dtype=torch.int64),
+                "target_tokens": torch.randint(1, 5, (2, 3)) if i != 2 else torch.zeros(2, 3, dtype=torch.int64)}
+               for i in range(4)]
+    with pytest.raises(TR.NonFiniteLossError, match="batch 3 .step index 2"):
+        TR.train_one_epoch(m, batches, opt, crit, "cpu", 1.0, None, 0, 0, None)
+    assert TR.train_one_epoch(m, batches[:2], opt, crit, "cpu", 1.0, None, 0, 0, None) > 0
