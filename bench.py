@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
-PMC_SUMMARY = "r03_pmc.json"
+PMC_SUMMARIES = ("r04_pmc.json", "r03_pmc.json")  # the newest committed PMC summary is used
 METRIC = "image-caption pairs/sec (train step), 6L/d512 decoder + ViT-B/16, 1/2/4/8 GPU"
 
 
@@ -166,24 +166,46 @@ class GemmProbe:
         return out
 
 
+def _pmc_summary():
+    for name in PMC_SUMMARIES:
+        path = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(path) as f:
+                return json.load(f), f"profiles/{name}"
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
 def pmc_traffic(kernel_prefix):
     """HBM bytes per launch of a kernel (averaged over the launches of all its template instances)
-    from the committed rocprofv3 PMC summary (FETCH_SIZE and
-    WRITE_SIZE passes of tools/profile_round.sh over this same command, condensed by
-    tools/rocpd_summary.py); None when no summary is present."""
-    path = os.path.join(ROOT, "profiles", PMC_SUMMARY)
-    try:
-        with open(path) as f:
-            ks = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
+    from the committed rocprofv3 PMC summary (FETCH_SIZE and WRITE_SIZE passes of
+    tools/profile_round.sh over this same command, condensed by tools/rocpd_summary.py); None when no
+    summary is present."""
+    d, src = _pmc_summary()
+    if d is None:
         return None, None
-    # every template instance of the kernel (activation / dropout variants), launch-weighted
     tot, n = 0.0, 0
-    for name, e in ks.items():
+    for name, e in d.get("kernels", {}).items():
         if name.startswith(kernel_prefix) and "hbm_bytes_per_launch" in e:
             tot += e["hbm_bytes_per_launch"] * e["launches"]
             n += e["launches"]
-    return (round(tot / n), f"profiles/{PMC_SUMMARY}") if n else (None, None)
+    return (round(tot / n), src) if n else (None, None)
+
+
+def pmc_mfma(kernel_prefix):
+    """(MFMA-busy fraction, effective clock GHz) of a kernel, launch-weighted over its instances, from the
+    MFMA-busy pass of the same summary (SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE, tools/rocpd_summary.py)."""
+    d, src = _pmc_summary()
+    ks = (d or {}).get("mfma_pass", {}).get("kernels", {})
+    busy = clk = 0.0
+    n = 0
+    for name, e in ks.items():
+        if name.startswith(kernel_prefix) and "mfma_busy_frac" in e:
+            busy += e["mfma_busy_frac"] * e["launches"]
+            clk += e["eff_clock_ghz"] * e["launches"]
+            n += e["launches"]
+    return (round(busy / n, 4), round(clk / n, 3), src) if n else (None, None, None)
 
 
 # Train workloads: BASELINE.json configs[1] (the metric's config, the default) and the single-GPU
@@ -582,18 +604,26 @@ def main():
                 return "gemm_bf16_grouped (TN: a decoder layer's six dW, one launch + split-K combine)"
             return f"{k[0]}<{k[1]},{k[2]}> ({role[(k[1], k[2])]})"
         key = max(agg, key=lambda k: agg[k][0])
-        t, fl, n, nb = agg[key]
+        # achieved: the launches as they ran INSIDE the steps (an event pair around each, the other streams'
+        # kernels sharing the chip) -- what rocprofv3's per-dispatch average of the same run sees; the
+        # isolated back-to-back replay of the same launches is reported beside it
+        t, fl, n, nb = inplace[key]
         ach = fl / t / 1e12
+        tr, flr, nr, _ = agg[key]
         # the committed PMC summary was collected on configs[1]; other workloads report no traffic
         traffic, src = (pmc_traffic(f"{key[0]}<{key[1]}, {key[2]},") if args.workload == "train" else (None, None))
+        busy, clk, bsrc = (pmc_mfma(f"{key[0]}<{key[1]}, {key[2]},") if args.workload == "train" else (None, None, None))
         out["roofline"] = {"bound": "mfma", "kernel": names(key), "achieved": round(ach, 1),
                            "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
                            "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": src,
+                           "mfma_busy": busy, "eff_clock_ghz": clk, "mfma_busy_source": bsrc,
                            "algorithmic_bytes_per_launch": round(nb / n), "flop_per_launch": round(fl / n),
                            "launches": n, "avg_launch_us": round(1e6 * t / n, 2),
-                           "avg_launch_us_event_bracketed": round(1e6 * inplace[key][0] / inplace[key][2], 2),
-                           "timing": "one step's launches of this kernel replayed in order, back-to-back, 3 passes, "
-                                     "between fence-free HIP events on the launch stream"}
+                           "avg_launch_us_isolated_replay": round(1e6 * tr / nr, 2),
+                           "achieved_isolated_replay": round(flr / tr / 1e12, 1),
+                           "timing": "every launch of this kernel in the last min(steps, 5) eager steps, each between "
+                                     "fence-free HIP events on its launch stream (the step's other streams running); "
+                                     "isolated replay: one step's launches re-issued back-to-back, 3 passes"}
         out["gemm_breakdown"] = {names(k): {"tflops": round(v[1] / v[0] / 1e12, 1),
                                                         "ms_per_step": round(1e3 * v[0] * inplace[k][2] / v[2] / min(args.steps, 5), 3)}
                                  for k, v in agg.items()}

@@ -101,6 +101,19 @@ typedef struct {
   float* rowsum;
   void* workspace;
   long workspace_bytes;
+  /* LayerNorm folded into the GEMM (the frozen encoder's pre-LN sublayers, encoder.py): A holds the raw
+   * rows x of LN(x) = (x - mean) rstd gamma + beta, B = W o gamma (the folded weight), bias = b + W beta,
+   * ln_colsum[n] = sum_k B(k, n): C = rstd_m (sum_k x_mk B_kn - mean_m ln_colsum_n) + bias_n, then the
+   * activation; (mean_m, rstd_m) merged from ln_stats [M][ln_parts][2] = per-64-column (mean, M2) of
+   * each row (ln_parts = K / 64), eps ln_eps. NULL: off. */
+  const float* ln_stats;
+  const float* ln_colsum;
+  int ln_parts;
+  float ln_eps;
+  /* stats_out (f32 [M][N / 64][2], NULL: off): per-64-column (mean, M2) of each bf16-rounded output row
+   * (the next LayerNorm's ln_stats). Both need bf16 NT operands and a plain bf16 vector epilogue
+   * (stats_out: a residual, no activation); they run on the 256x256 tile kernel. */
+  float* stats_out;
 } mit_gemm_args;
 int mit_gemm(const mit_gemm_args* args, void* stream);
 long mit_gemm_workspace_bytes(long M, long N, long K);
@@ -167,6 +180,11 @@ int mit_layernorm_bwd(int dtype, long rows, long cols, const void* dy, const voi
                       const float* rstd, const float* gamma, void* dx, void* dr, float r_drop_p, const uint64_t* seed,
                       uint32_t site, float* dgamma, float* dbeta, float* ws, void* stream);
 int mit_layernorm_param_grads(long rows, long cols, const float* ws, float* dgamma, float* dbeta, void* stream);
+/* Per-64-column (mean, M2) of each bf16 row: out[r][c / 64] = (mean, sum of squared deviations) over
+ * columns c .. c + 63 (cols % 64 == 0): the ln_stats of a LayerNorm-folded GEMM (mit_gemm) whose input
+ * rows no producer GEMM annotated (the encoder's embeddings). Replaces the statistics half of
+ * nn.LayerNorm at modeling_vit.py:274 for layer 0. */
+int mit_row_stats64(long rows, long cols, const void* x, long ldx, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Scaled-dot-product attention, head_dim Dh in {16, 32, 64, 128} (MFMA kernels at 64, generic

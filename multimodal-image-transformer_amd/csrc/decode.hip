@@ -142,6 +142,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(long H, const T* __res
 // rows contiguously (the (b, h)-block kernel reads 128-B pieces of every row, 8 times per DRAM page)
 // with U rows per wave in flight before the first use. Wave w takes keys w*U .. w*U+U-1 (+8U per
 // iteration); the 8 waves' softmax states merge once in LDS.
+// sum over the LPH (2 / 4 / 8 / 16) consecutive lanes of a head by DPP: quad_perm [1,0,3,2] and
+// [2,3,0,1], then row_half_mirror (lane i <-> 7 - i: the other quad's sum) and row_mirror (i <-> 15 - i)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int LPH>
+__device__ __forceinline__ float head_sum(float v) {
+  if constexpr (LPH >= 2) v += dpp_f<0xB1>(v);
+  if constexpr (LPH >= 4) v += dpp_f<0x4E>(v);
+  if constexpr (LPH >= 8) v += dpp_f<0x141>(v);
+  if constexpr (LPH >= 16) v += dpp_f<0x140>(v);
+  return v;
+}
+
 template <int DH, int U>
 __global__ __launch_bounds__(512) void attn_decode_rows_kernel(const bf16* __restrict__ q, long q_batch,
                                                                const bf16* __restrict__ k, long k_row, long k_batch,
@@ -163,6 +178,9 @@ __global__ __launch_bounds__(512) void attn_decode_rows_kernel(const bf16* __res
   const bf16* vb = v + b * v_batch + lane * 8;
   const int64_t* tb = key_tokens ? key_tokens + b * tok_batch : nullptr;
   float m = kNegBig, l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // the U keys of an iteration as ONE online-softmax block: the U scores are independent (dot products
+  // and head reductions pipeline), one max / one rescale per block and one exp2 per key (was a dependent
+  // max -> 2 exp2 -> rescale chain per key); head reductions over the LPH lanes by DPP within the row
   for (long j0 = (long)w * U; j0 < Lk; j0 += 8 * U) {
     bf16x8 kr[U], vr[U];
     bool ok[U];
@@ -181,21 +199,35 @@ __global__ __launch_bounds__(512) void attn_decode_rows_kernel(const bf16* __res
 #pragma unroll
       for (int u = 0; u < U; ++u) ok[u] = ok[u] && tb[j0 + u] != pad_idx;
     }
+    float s[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      float s = 0.f;
+      float t = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) s = fmaf(qv[i], (float)kr[u][i], s);
-#pragma unroll
-      for (int x = 1; x < LPH; x <<= 1) s += __shfl_xor(s, x, 64);
-      if (!ok[u]) s = -INFINITY;
-      const float mn = fmaxf(m, s);
-      const float corr = exp2f(m - mn), p = exp2f(s - mn);
-      l = l * corr + p;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = fmaf(p, (float)vr[u][i], acc[i] * corr);
-      m = mn;
+      for (int i = 0; i < 8; ++i) t = fmaf(qv[i], (float)kr[u][i], t);
+      s[u] = t;
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[u] = head_sum<LPH>(s[u]);
+    float bm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) s[u] = -INFINITY;
+      bm = fmaxf(bm, s[u]);
+    }
+    const float mn = fmaxf(m, bm);
+    const float corr = exp2f(m - mn);
+    l *= corr;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] *= corr;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float p = exp2f(s[u] - mn);
+      l += p;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(p, (float)vr[u][i], acc[i]);
+    }
+    m = mn;
   }
   float* mine = red[w][lane];
   mine[0] = m;
@@ -257,11 +289,36 @@ __global__ __launch_bounds__(256) void greedy_pick_kernel(long V, const float* _
   };
   float best = -INFINITY;
   long bi = V;  // V = none yet (loses every tie on index)
-  for (long j = threadIdx.x; j < V; j += blockDim.x) {
-    const float x = row[j];
-    if (better(x, j, best, bi)) {
-      best = x;
-      bi = j;
+  if ((V & 3) == 0 && (ld & 3) == 0 && ((uintptr_t)logits & 15) == 0) {
+    // 16-B loads, 4 per thread in flight before the first compare (the scalar loop was one dependent
+    // load round trip per 256 logits: 18 us for a 256 x 10000 step)
+    const long nv = V >> 2;
+    const f32x4* r4 = (const f32x4*)row;
+    for (long i0 = threadIdx.x; i0 < nv; i0 += 4L * blockDim.x) {
+      f32x4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long i = i0 + (long)u * blockDim.x;
+        x[u] = i < nv ? r4[i] : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const long j = 4 * (i0 + (long)u * blockDim.x) + t;
+          if (j < V && better(x[u][t], j, best, bi)) {
+            best = x[u][t];
+            bi = j;
+          }
+        }
+    }
+  } else {
+    for (long j = threadIdx.x; j < V; j += blockDim.x) {
+      const float x = row[j];
+      if (better(x, j, best, bi)) {
+        best = x;
+        bi = j;
+      }
     }
   }
 #pragma unroll

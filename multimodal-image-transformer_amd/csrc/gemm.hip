@@ -55,6 +55,14 @@ struct Epi {
   float dscale;
   int dropout;
   int vec;  // 16-B vector epilogue legal (alignments / leading dims / N multiple of 8)
+  // LayerNorm folded into the GEMM (256 kernel, STG 3): A = the raw rows x, the epilogue applies
+  // rstd_m (acc - mean_m colsum_n) + bias_n with (mean, rstd) merged from ln_stats [M][ln_parts][2]
+  const float* ln_stats;
+  const float* ln_colsum;
+  int ln_parts;
+  float ln_eps;
+  // per-64-column (mean, M2) of each output row (256 kernel, STG 4): stats_out [M][N / 64][2]
+  float* stats_out;
 };
 
 constexpr int ACT_RT = -1;
@@ -738,7 +746,40 @@ __device__ __forceinline__ void reg_epilogue(const f32x4 (&acc)[MI][4], const Ep
 // 5.9 -> 4.8 us; enc qkv+bias 51.1 -> 48.8 us, fc1 73.8 -> 68.8, kv_all 102 -> 94.7; residual loads as
 // 8-B segments in the accumulator layout instead: slower (o+res 28.6 -> 31.9 us). Image: row r at
 // r * 128 B, 16-B chunk c at (c ^ (r & 7)) * 16 (the 8-row x 8-chunk read-back is conflict-free).
-template <int ACT, bool DROP, bool XOPS>
+// Chan merge of two (count, mean, M2) row aggregates in a fixed order (a, then b): every lane that
+// merges the same pair gets the same bits
+__device__ __forceinline__ void chan_merge(float& n, float& m, float& q, float na, float ma, float qa, float nb, float mb,
+                                           float qb) {
+  const float nt = na + nb, d = mb - ma, f = nt > 0.f ? nb / nt : 0.f;
+  n = nt;
+  m = ma + d * f;
+  q = qa + qb + d * d * na * f;
+}
+// (count, mean, M2) over the 4 lane groups of a row (lanes l, l^16, l^32, l^48): v_permlane16_swap /
+// v_permlane32_swap of a value with itself return the pair's lower-group value first, so both lanes of a
+// pair merge in the same order
+__device__ __forceinline__ void chan_merge_rows(float& n, float& m, float& q) {
+  auto sw16 = [](float x) { return __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false); };
+  auto sw32 = [](float x) { return __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false); };
+  const auto a = sw16(n), b = sw16(m), c = sw16(q);
+  chan_merge(n, m, q, __uint_as_float(a[0]), __uint_as_float(b[0]), __uint_as_float(c[0]), __uint_as_float(a[1]),
+             __uint_as_float(b[1]), __uint_as_float(c[1]));
+  const auto a2 = sw32(n), b2 = sw32(m), c2 = sw32(q);
+  chan_merge(n, m, q, __uint_as_float(a2[0]), __uint_as_float(b2[0]), __uint_as_float(c2[0]), __uint_as_float(a2[1]),
+             __uint_as_float(b2[1]), __uint_as_float(c2[1]));
+}
+__device__ __forceinline__ float sum_rows(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// LNX: 0 = plain; 1 = LayerNorm-folded operand (the wave's rows' (mean, rstd) merged from e.ln_stats:
+// lane group g takes partials g, g+4, g+8, g+12, then chan_merge_rows; v = rstd (acc - mean colsum) +
+// bias); 2 = also write the per-64-column (mean, M2) of the bf16-rounded output rows to e.stats_out
+// (the next LayerNorm's statistics: this wave's 64 columns are one partial)
+template <int ACT, bool DROP, bool XOPS, int LNX = 0>
 __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const Epi& e, void* C, long ldc, long M,
                                                long N, long mw, long nw, int lane, char* stg) {
   constexpr int PASSES = 1, IP = 8;  // one pass over the wave's 8 16-row blocks
@@ -752,6 +793,25 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
       bj[j][0] = b[0]; bj[j][1] = b[1]; bj[j][2] = b[2]; bj[j][3] = b[3];
     } else {
       bj[j][0] = bj[j][1] = bj[j][2] = bj[j][3] = 0.f;
+    }
+  }
+  float sj[LNX == 1 ? 4 : 1][4];  // LN fold: the column sums of the folded weight rows
+  f32x2 lp[LNX == 1 ? 8 : 1][4];  // LN fold: this lane's statistics partials of its 8 rows
+  if constexpr (LNX == 1) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long c = nw + 16 * j + 4 * g;
+      const f32x4 b = c < N ? *(const f32x4*)(e.ln_colsum + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      sj[j][0] = b[0]; sj[j][1] = b[1]; sj[j][2] = b[2]; sj[j][3] = b[3];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long row = mw + 16 * i + r16;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int pi = g + 4 * u;
+        lp[i][u] = (row < M && pi < e.ln_parts) ? *(const f32x2*)(e.ln_stats + (row * e.ln_parts + pi) * 2) : f32x2{0.f, 0.f};
+      }
     }
   }
   typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
@@ -771,6 +831,31 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
   }
   gather_wait();
   const uint64_t key = epi_key<DROP>(e);
+  float rs_i[LNX == 1 ? 8 : 1], nr_i[LNX == 1 ? 8 : 1];  // rstd, -rstd * mean of the lane's 8 rows
+  if constexpr (LNX == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float s = 0.f, cnt = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (g + 4 * u < e.ln_parts) {
+          s += lp[i][u][0];
+          cnt += 1.f;
+        }
+      float m = cnt > 0.f ? s / cnt : 0.f, q = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (g + 4 * u < e.ln_parts) {
+          const float d = lp[i][u][0] - m;
+          q += lp[i][u][1] + 64.f * d * d;
+        }
+      float n = 64.f * cnt;
+      chan_merge_rows(n, m, q);
+      const float rs = __builtin_amdgcn_rsqf(q / n + e.ln_eps);
+      rs_i[i] = rs;
+      nr_i[i] = -rs * m;
+    }
+  }
 #pragma unroll
   for (int ps = 0; ps < PASSES; ++ps) {
     if constexpr (XOPS) {
@@ -785,11 +870,18 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
       const int i = ps * IP + ii;
       const int rr = 16 * ii + r16;  // row in the image
       const long row = mw + 16 * i + r16;
+      float st_s = 0.f;
+      float vr[LNX == 2 ? 4 : 1][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float v[4];
+        if constexpr (LNX == 1) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t] * e.alpha + bj[j][t];
+          for (int t = 0; t < 4; ++t) v[t] = fmaf(acc[i][j][t], rs_i[i], fmaf(nr_i[i], sj[j][t], bj[j][t]));
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t] * e.alpha + bj[j][t];
+        }
         if (ACT == MIT_ACT_GELU) {
 #pragma unroll
           for (int t = 0; t < 4; t += 2) {
@@ -832,6 +924,23 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
         typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
         const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         *(bf16x4*)seg = o;
+        if constexpr (LNX == 2) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            vr[j][t] = (float)o[t];
+            st_s += vr[j][t];
+          }
+        }
+      }
+      if constexpr (LNX == 2) {  // (mean, M2) of the row's 64 columns nw .. nw + 63 (two passes)
+        const float mean = sum_rows(st_s) * (1.f / 64.f);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) q += (vr[j][t] - mean) * (vr[j][t] - mean);
+        q = sum_rows(q);
+        if (g == 0 && row < M) *(f32x2*)(e.stats_out + (row * (N >> 6) + (nw >> 6)) * 2) = f32x2{mean, q};
       }
     }
 #pragma unroll
@@ -845,7 +954,8 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
 }
 
 // STG (bf16 out, gathered epilogue, K-contig A): 1 = the LDS-staged epilogue without operands, 2 = with
-// the residual / aux block; 0 = the register (f32 out) or LDS-stage (MN-contig A) epilogue. A template
+// the residual / aux block, 3 = LayerNorm-folded A (no operand), 4 = residual + the output rows'
+// per-64-column statistics; 0 = the register (f32 out) or LDS-stage (MN-contig A) epilogue. A template
 // flag, not a run-time branch: two epilogues in one instance spill in the K loop.
 template <int ALAY, int BLAY, int ACT, bool DROP, int STG = 0>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* C,
@@ -1018,7 +1128,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
         // ago), group 1 into the last K-tile's buffer (every read of it returned by the last barrier)
         const int buf = wr == 0 ? (nk & 1) : ((nk - 1) & 1);
         char* stg = smem + buf * BUF_BYTES + wc * 16384;
-        stage_epilogue<ACT, DROP, STG == 2>(acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane, stg);
+        stage_epilogue<ACT, DROP, STG == 2 || STG == 4, STG == 3 ? 1 : (STG == 4 ? 2 : 0)>(
+            acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane, stg);
         return;
       }
     }
@@ -1424,9 +1535,31 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
       set_lds(gemm256_kernel<AL, BL, ACT, DROP, 1>, SMEM2_BYTES);
       if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 2>, SMEM2_BYTES);
     }
+    if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
+      if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 4>, SMEM2_BYTES);
+      if constexpr (!DROP) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 3>, SMEM2_BYTES);
+    }
     attr = true;
   }
   const dim3 grid((unsigned)(nbm * nbn));
+  if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {  // LayerNorm fold / statistics (mit_gemm checked them)
+    if constexpr (!DROP) {
+      if (e.ln_stats) {
+        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 3>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+                           (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
+                           (float*)g->workspace, g->rowsum);
+        return;
+      }
+    }
+    if constexpr (ACT == MIT_ACT_NONE) {
+      if (e.stats_out) {
+        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 4>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+                           (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
+                           (float*)g->workspace, g->rowsum);
+        return;
+      }
+    }
+  }
   if constexpr (AL == MIT_K_CONTIG) {
     const bool ops = e.res || e.aux;
     if (epi_gatherable(e) && !e.out_f32) {
@@ -1457,7 +1590,7 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
 // kernel's LDS tiles): 2.5-3x slower on the M = 4032 decoder shapes, 2x on the decode fc_out
 // (tools/blas_reference.py)
 bool use_rs(const mit_gemm_args* g) {
-  if (g->a_layout != MIT_K_CONTIG || g->b_layout != MIT_K_CONTIG || g->rowsum) return false;
+  if (g->a_layout != MIT_K_CONTIG || g->b_layout != MIT_K_CONTIG || g->rowsum || g->ln_stats || g->stats_out) return false;
   const int v = gemm_variant();
   if (v == 3) return true;
   if (v != 0) return false;
@@ -1583,8 +1716,8 @@ extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
   const Split sp = plan_split(g);
   if (ksplit) *ksplit = sp.ks;
   if (sp.ks == 1 && use_rs(g)) return 65;  // the 64x64 register-streaming kernel
-  const bool big = sp.ks == 1 && use_256(g->M, g->N, g->K, g->a_layout) && epi_kind(g) != EK_GENERIC &&
-                   (g->act == MIT_ACT_NONE || (!g->residual && !g->aux));
+  const bool big = sp.ks == 1 && (use_256(g->M, g->N, g->K, g->a_layout) || g->ln_stats || g->stats_out) &&
+                   epi_kind(g) != EK_GENERIC && (g->act == MIT_ACT_NONE || (!g->residual && !g->aux));
   return big ? 256 : 128;
 }
 
@@ -1618,7 +1751,29 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
     if (g->K == 0) a_bytes = b_bytes = 0;
     MIT_CHECK_ARG(a_bytes < (1L << 31) && b_bytes < (1L << 31), "mit_gemm(bf16): operand spans >= 2 GiB");
   }
+  if (g->ln_stats || g->stats_out) {
+    // the LayerNorm fold / row statistics exist only in the 256 kernel's LDS-staged bf16 epilogue
+    MIT_CHECK_ARG(g->dtype == MIT_BF16 && g->a_layout == MIT_K_CONTIG && g->b_layout == MIT_K_CONTIG && !g->out_f32 &&
+                      !g->accumulate && !g->aux && g->drop_p <= 0.f && g->alpha == 1.0f && !g->rowsum && !g->workspace &&
+                      g->N % 8 == 0 && g->ldc % 8 == 0 && al16(g->C) && (!g->bias || al16(g->bias)),
+                  "mit_gemm: ln_stats / stats_out need bf16 NT operands, a bf16 output with a plain vector epilogue");
+    MIT_CHECK_ARG(!(g->ln_stats && g->stats_out), "mit_gemm: ln_stats and stats_out are exclusive");
+  }
+  if (g->ln_stats) {
+    MIT_CHECK_ARG(g->ln_colsum && al16(g->ln_colsum) && g->K % 64 == 0 && g->ln_parts == g->K / 64 && g->ln_parts <= 16 &&
+                      !g->residual && g->ln_eps >= 0.f,
+                  "mit_gemm: ln_stats needs ln_colsum (16-B aligned), K %% 64 == 0, ln_parts = K / 64 <= 16, no residual");
+  }
+  if (g->stats_out) {
+    MIT_CHECK_ARG(g->N % 64 == 0 && g->act == MIT_ACT_NONE && g->residual && g->ldr % 8 == 0 && al16(g->residual),
+                  "mit_gemm: stats_out needs N %% 64 == 0, no activation and a (16-B aligned) residual");
+  }
   Epi e;
+  e.ln_stats = g->ln_stats;
+  e.ln_colsum = g->ln_colsum;
+  e.ln_parts = g->ln_parts;
+  e.ln_eps = g->ln_eps;
+  e.stats_out = g->stats_out;
   e.bias = g->bias;
   e.res = g->residual;
   e.ldr = g->ldr;
@@ -1640,7 +1795,7 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   if (g->dtype == MIT_BF16) {
     const int ab = (int)a_bytes, bb = (int)b_bytes;
     const Split sp = plan_split(g);
-    const bool big = sp.ks == 1 && use_256(g->M, g->N, g->K, g->a_layout);
+    const bool big = sp.ks == 1 && (use_256(g->M, g->N, g->K, g->a_layout) || g->ln_stats || g->stats_out);
     if (g->a_layout == 0 && g->b_layout == 0) launch_layout<0, 0>(g, e, ab, bb, sp, big, s);
     else if (g->a_layout == 0 && g->b_layout == 1) launch_layout<0, 1>(g, e, ab, bb, sp, big, s);
     else if (g->a_layout == 1 && g->b_layout == 0) launch_layout<1, 0>(g, e, ab, bb, sp, big, s);

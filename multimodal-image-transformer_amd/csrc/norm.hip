@@ -830,3 +830,49 @@ extern "C" int mit_layernorm_param_grads(long rows, long cols, const float* ws, 
   MIT_LAUNCH_CHECK("mit_layernorm_param_grads");
   return MIT_OK;
 }
+
+namespace {
+// per-64-column (mean, M2) of each bf16 row: 8 lanes per 64-column chunk (8 bf16 each, one 16-B load),
+// reductions over the chunk's 8 lanes by shuffles, two passes (mean, then squared deviations); one wave per
+// row, 512 columns per wave pass
+__global__ __launch_bounds__(256) void row_stats64_kernel(long rows, long cols, const bf16* __restrict__ x, long ldx,
+                                                          float* __restrict__ out) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const long P = cols / 64;
+  for (long c = 8L * lane; c - 8L * lane < cols; c += 512) {
+    float v[8];
+    const bool ok = c < cols;
+    if (ok) ld8(x + r * ldx + c, v);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += ok ? v[k] : 0.f;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s * (1.f / 64.f);
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q += ok ? (v[k] - mean) * (v[k] - mean) : 0.f;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) q += __shfl_xor(q, o, 64);
+    if (ok && (lane & 7) == 0) {
+      float* dst = out + (r * P + c / 64) * 2;
+      dst[0] = mean;
+      dst[1] = q;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int mit_row_stats64(long rows, long cols, const void* x, long ldx, float* out, void* stream) {
+  MIT_RECORD([=]() { return mit_row_stats64(rows, cols, x, ldx, out, stream); });
+  MIT_CHECK_ARG(x && out, "mit_row_stats64: null pointer");
+  MIT_CHECK_ARG(cols > 0 && cols % 64 == 0 && ldx >= cols && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0,
+                "mit_row_stats64: cols %% 64 == 0, ldx %% 8 == 0, 16-B aligned rows");
+  if (rows <= 0) return MIT_OK;
+  hipLaunchKernelGGL(row_stats64_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, rows, cols,
+                     (const bf16*)x, ldx, out);
+  MIT_LAUNCH_CHECK("mit_row_stats64");
+  return MIT_OK;
+}

@@ -72,6 +72,9 @@ class VisionEncoder:
         # f32 residual stream (bf16 compute only): z = h + sublayer(bf16) in f32, fused into the next
         # LayerNorm (mit_layernorm_fwd_x32), as autocast keeps modeling_vit.py:312-323 / modeling_clip.py:379-393
         self.res32 = dtype == torch.bfloat16 and (mode in ("on", "1", "true") or (mode == "auto" and self.L >= 24))
+        # bf16 stream: each pre-LN sublayer's LayerNorm folded into the GEMM that consumes it (fold_layernorm):
+        # no LayerNorm launch inside the tower, the statistics come from the producing GEMM's epilogue
+        self.fold_ln = dtype == torch.bfloat16 and not self.res32 and self.E % 64 == 0
         self.w: Dict[str, torch.Tensor] = {}
         self._ws = {}
 
@@ -151,6 +154,13 @@ class VisionEncoder:
         for k, v in w.items():
             is_mat = k.endswith(".w") and v.dim() == 2 and not k.endswith("ln.w")
             out[k] = v.to(device=dev, dtype=dt if is_mat else torch.float32).contiguous()
+        if self.fold_ln:
+            for i in range(self.L):
+                for mat, ln in (("qkv", "ln1"), ("fc1", "ln2")):
+                    wf, bf, sf = fold_layernorm(w[f"{i}.{mat}.w"], w[f"{i}.{mat}.b"], w[f"{i}.{ln}.w"], w[f"{i}.{ln}.b"])
+                    out[f"{i}.{mat}.wf"] = wf.to(dev).contiguous()
+                    out[f"{i}.{mat}.bf"] = bf.to(dev).contiguous()
+                    out[f"{i}.{mat}.sf"] = sf.to(dev).contiguous()
         self.w = out
         old = getattr(self, "extra", {})
         self.extra = {k: extra.get(k, old.get(k, torch.zeros(shp))) for k, shp in self._extra_shapes().items()}
@@ -250,6 +260,8 @@ class VisionEncoder:
                 m=torch.empty(R, self.mlp, dtype=dt, device=dev),
                 out=torch.empty(R, E, dtype=dt, device=dev),
             )
+            if self.fold_ln:  # per-64-column (mean, M2) of the residual stream's rows
+                self._ws[key]["st"] = torch.empty(R, E // 64, 2, dtype=torch.float32, device=dev)
             if self.res32:  # f32 residual stream, the bf16 sublayer output (delta) and CLIP's f32 embeddings
                 ws = self._ws[key]
                 ws["h32"] = torch.empty(R, E, dtype=torch.float32, device=dev)
@@ -266,8 +278,7 @@ class VisionEncoder:
 
     def forward_split(self, images: torch.Tensor, rows: str = "all", slot: int = 0, split: int = 0):
         """Launches the patch embedding and layers [0, split) now; returns rest() which launches
-        layers [split, L) and the final LayerNorm and returns forward()'s result. The prefetch stream
-        uses it to spread the frozen encoder over a step (model.prefetch_encoder)."""
+        layers [split, L) and the final LayerNorm and returns forward()'s result (forward: split = L)."""
         B = images.shape[0]
         if tuple(images.shape[1:]) != (3, self.image, self.image):
             raise ValueError(f"expected images [B,3,{self.image},{self.image}], got {tuple(images.shape)}")
@@ -286,10 +297,10 @@ class VisionEncoder:
             h, ws["a"] = ws["a"], h  # swap roles: the normalised tensor is the residual stream
             ws["h"] = h
         a, qkv, o, m = ws["a"], ws["qkv"], ws["o"], ws["m"]
-        self._layers(B, h, a, qkv, o, m, act, 0, split)
+        self._layers(B, h, a, qkv, o, m, act, 0, split, ws.get("st"))
 
         def rest():
-            self._layers(B, h, a, qkv, o, m, act, split, self.L)
+            self._layers(B, h, a, qkv, o, m, act, split, self.L, ws.get("st"))
             return self._finish(B, ws, h, rows)
         return rest
 
@@ -300,8 +311,10 @@ class VisionEncoder:
                                 N * 3 * E, o, E, N * E, scale=1.0 / math.sqrt(self.hd))
         native.attention_fwd(native.dtype_code(qkv), B, H, N, N, args, Dh=self.hd)
 
-    def _layers(self, B, h, a, qkv, o, m, act, i0, i1):
+    def _layers(self, B, h, a, qkv, o, m, act, i0, i1, st=None):
         w = self.w
+        if self.fold_ln:
+            return self._layers_folded(B, h, qkv, o, m, act, i0, i1, st)
         for i in range(i0, i1):
             native.layernorm_fwd(h, w[f"{i}.ln1.w"], w[f"{i}.ln1.b"], self.eps, a)
             self._attention(B, a, qkv, o, i)
@@ -309,6 +322,26 @@ class VisionEncoder:
             native.layernorm_fwd(h, w[f"{i}.ln2.w"], w[f"{i}.ln2.b"], self.eps, a)
             native.linear(a, w[f"{i}.fc1.w"], m, bias=w[f"{i}.fc1.b"], act=act)
             native.linear(m, w[f"{i}.fc2.w"], h, bias=w[f"{i}.fc2.b"], residual=h)
+
+    def _layers_folded(self, B, h, qkv, o, m, act, i0, i1, st):
+        """The bf16-stream layers with every LayerNorm folded into its consumer GEMM (mit_gemm ln_stats): the
+        qkv and fc1 GEMMs read the raw residual stream h and normalise in the epilogue from per-64-column
+        row statistics, which the o-proj / fc2 residual GEMMs write for the h they produce (stats_out);
+        layer 0's come from one mit_row_stats64 pass over the embeddings. 5 launches per layer instead of 7,
+        no LayerNorm output round trip through HBM (2 x 19 MB per LayerNorm at ViT-B/16, B = 64)."""
+        w, E, R = self.w, self.E, B * self.N
+        if i0 == 0:
+            native.row_stats64(h, st)
+        for i in range(i0, i1):
+            native.gemm(h, w[f"{i}.qkv.wf"], qkv, R, 3 * E, E, bias=w[f"{i}.qkv.bf"], ln_stats=st,
+                        ln_colsum=w[f"{i}.qkv.sf"], ln_eps=self.eps)
+            args = native.attn_args(qkv, 3 * E, self.N * 3 * E, qkv[:, E:], 3 * E, self.N * 3 * E, qkv[:, 2 * E:], 3 * E,
+                                    self.N * 3 * E, o, E, self.N * E, scale=1.0 / math.sqrt(self.hd))
+            native.attention_fwd(native.dtype_code(qkv), B, self.H, self.N, self.N, args, Dh=self.hd)
+            native.gemm(o, w[f"{i}.o.w"], h, R, E, E, bias=w[f"{i}.o.b"], residual=h, stats_out=st)
+            native.gemm(h, w[f"{i}.fc1.wf"], m, R, self.mlp, E, bias=w[f"{i}.fc1.bf"], act=act, ln_stats=st,
+                        ln_colsum=w[f"{i}.fc1.sf"], ln_eps=self.eps)
+            native.gemm(m, w[f"{i}.fc2.w"], h, R, E, self.mlp, bias=w[f"{i}.fc2.b"], residual=h, stats_out=st)
 
     def _forward_res32(self, B, ws, rows, act, split):
         """The same forward with the residual stream h32 in f32: every sublayer output (o-proj, fc2)
@@ -376,6 +409,19 @@ class VisionEncoder:
         N, E, m = self.N, self.E, self.mlp
         per_layer = 2 * N * 4 * E * E + 2 * N * 2 * E * m + 4 * N * N * E
         return self.L * per_layer + 2 * (N - 1) * E * self.kin
+
+
+def fold_layernorm(W: torch.Tensor, b: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor):
+    """A pre-LN sublayer y = LN(x) W^T + b with LN(x) = (x - mean) rstd gamma + beta, rewritten for a GEMM on
+    the raw rows x (mit_gemm ln_stats): y = rstd (x (W o gamma)^T - mean s) + (b + W beta), s_n = sum_k
+    (W o gamma)_nk. Returns (W o gamma in bf16 -- what the GEMM reads --, the folded bias f32, s f32 summed
+    from the bf16-rounded weights so the mean term cancels exactly what the GEMM accumulates). The frozen
+    encoder's weights never change, so this runs once at load (encoder.py:load_hf_state_dict)."""
+    W64, g64 = W.double(), gamma.double()
+    wf = (W64 * g64[None, :]).to(torch.bfloat16)
+    s = wf.double().sum(1).float()
+    bf = (b.double() + W64 @ beta.double()).float()
+    return wf, bf, s
 
 
 def get_encoder_output_dim(name: Optional[str] = None) -> int:

@@ -43,7 +43,8 @@ class GemmArgs(ctypes.Structure):
                 ("A", vp), ("lda", L), ("B", vp), ("ldb", L), ("C", vp), ("ldc", L), ("alpha", Fl),
                 ("bias", vp), ("act", I), ("residual", vp), ("ldr", L), ("aux", vp), ("ld_aux", L),
                 ("aux_scale", Fl), ("drop_p", Fl), ("seed", vp), ("site", U32), ("out_f32", I),
-                ("accumulate", I), ("rowsum", vp), ("workspace", vp), ("workspace_bytes", L)]
+                ("accumulate", I), ("rowsum", vp), ("workspace", vp), ("workspace_bytes", L),
+                ("ln_stats", vp), ("ln_colsum", vp), ("ln_parts", I), ("ln_eps", Fl), ("stats_out", vp)]
 
 
 class DecodeGemmArgs(ctypes.Structure):
@@ -84,6 +85,7 @@ SIGNATURES = {
     "mit_layernorm_fwd": (I, [I, L, L, vp, L, vp, L, Fl, vp, U32, vp, vp, Fl, vp, vp, L, vp, vp, vp]),
     "mit_layernorm_fwd_x32": (I, [L, L, vp, L, vp, L, vp, vp, vp, Fl, vp, I, L, vp]),
     "mit_residual_out": (I, [L, L, vp, L, vp, L, vp, L, vp]),
+    "mit_row_stats64": (I, [L, L, vp, L, vp, vp]),
     "mit_layernorm_bwd_ws_floats": (L, [L, L]),
     "mit_layernorm_bwd": (I, [I, L, L, vp, vp, vp, vp, vp, vp, vp, Fl, vp, U32, vp, vp, vp, vp]),
     "mit_layernorm_param_grads": (I, [L, L, vp, vp, vp, vp]),
@@ -402,10 +404,13 @@ def dtype_code(t: torch.Tensor) -> int:
 # ------------------------------------------------------------------------------------------------
 def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ldb=None, ldc=None, bias=None,
          act=ACT_NONE, residual=None, ldr=None, aux=None, ld_aux=None, aux_scale=1.0, alpha=1.0, drop_p=0.0,
-         seed=None, site=0, accumulate=False, rowsum=None, workspace=None):
+         seed=None, site=0, accumulate=False, rowsum=None, workspace=None, ln_stats=None, ln_colsum=None, ln_eps=0.0,
+         stats_out=None):
     """C = epi(alpha * A(m,k) B(k,n)); see include/mit_hip.h. Output dtype = C.dtype (f32 or operand dtype).
     rowsum: optional f32 [M] <- sum_k A(m,k) (fused bias gradient); workspace: split-K scratch, zero-filled
-    once before first use (gemm_workspace(M, N, K)), one per stream."""
+    once before first use (gemm_workspace(M, N, K)), one per stream. ln_stats / ln_colsum / ln_eps: the
+    LayerNorm of A's rows folded in (B, bias already folded: encoder.fold_layernorm); stats_out: f32
+    [M, N / 64, 2] <- per-64-column (mean, M2) of the output rows."""
     dt = dtype_code(A)
     if B.dtype != A.dtype:
         raise NativeError("gemm: A and B dtypes differ")
@@ -421,7 +426,8 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
     g = GemmArgs(dt, a_layout, b_layout, M, N, K, ptr(A), lda, ptr(B), ldb, ptr(C), ldc, alpha, ptr(bias), act,
                  ptr(residual), ldr if ldr is not None else ldc, ptr(aux), ld_aux if ld_aux is not None else ldc,
                  aux_scale, drop_p, ptr(seed), site, out_f32, 1 if accumulate else 0, ptr(rowsum), ptr(workspace),
-                 0 if workspace is None else workspace.numel() * workspace.element_size())
+                 0 if workspace is None else workspace.numel() * workspace.element_size(), ptr(ln_stats),
+                 ptr(ln_colsum), K // 64 if ln_stats is not None else 0, ln_eps, ptr(stats_out))
     probe = _gemm_probe
     if probe is not None:
         # algorithmic bytes: operands once, output once (+ read-back of C / residual / aux when used)
@@ -538,6 +544,13 @@ def layernorm_fwd_x32(x, gamma, beta, eps, y, *, r=None, z=None, rows=None, cols
     rows = rows if rows is not None else x.numel() // cols
     _check(lib().mit_layernorm_fwd_x32(rows, cols, ptr(x), ldx or cols, ptr(r), ldr or cols, ptr(z), ptr(gamma), ptr(beta),
                                        eps, ptr(y), dtype_code(y), ldy or cols, stream_ptr()), "mit_layernorm_fwd_x32")
+
+
+def row_stats64(x, out, *, rows=None, cols=None, ldx=None):
+    """out f32 [rows, cols / 64, 2] <- per-64-column (mean, M2) of the bf16 rows of x (mit_row_stats64)."""
+    cols = cols if cols is not None else x.shape[-1]
+    rows = rows if rows is not None else x.numel() // cols
+    _check(lib().mit_row_stats64(rows, cols, ptr(x), ldx or cols, ptr(out), stream_ptr()), "mit_row_stats64")
 
 
 def residual_out(x, r, y, *, rows=None, cols=None, ldx=None, ldr=None, ldy=None):

@@ -161,3 +161,89 @@ def test_register_streaming_kernel(M, Nn, K):
     C2 = torch.empty_like(C)
     N.gemm(A, B, C2, M, Nn, K)
     assert torch.equal(C, C2), "register-streaming kernel not deterministic"
+
+
+def _stats64_ref(y):
+    """per-64-column (mean, M2) of each row, float64"""
+    R, C = y.shape
+    t = y.double().view(R, C // 64, 64)
+    m = t.mean(-1)
+    return torch.stack([m, ((t - m[..., None]) ** 2).sum(-1)], -1)
+
+
+def test_row_stats64_matches_torch():
+    R, C = 1003, 768
+    x = (3 * torch.randn(R, 2 * C, device=dev()) + 1).to(torch.bfloat16)
+    st = torch.empty(R, C // 64, 2, device=dev())
+    N.row_stats64(x, st, rows=R, cols=C, ldx=2 * C)
+    ref = _stats64_ref(x[:, :C])
+    assert (st.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("act", [0, 2])
+@pytest.mark.parametrize("M,Nn,K", [(1000, 2304, 768), (12608, 3072, 768), (300, 520, 256)])
+def test_gemm_layernorm_fold(M, Nn, K, act):
+    """LN(x) W^T + b computed as rstd (x (W o gamma)^T - mean colsum) + (b + W beta) in the 256 kernel's
+    epilogue (encoder.fold_layernorm + mit_gemm ln_stats) against float64 torch; no less accurate than the
+    LayerNorm kernel -> bf16 -> GEMM sequence it replaces."""
+    import torch.nn.functional as F
+    from encoder import fold_layernorm
+    torch.manual_seed(M + Nn)
+    x = (2 * torch.randn(M, K, device=dev()) + 0.5 * torch.randn(K, device=dev())).to(torch.bfloat16)
+    W = torch.randn(Nn, K) / K ** 0.5
+    b, gamma, beta = 0.1 * torch.randn(Nn), 1 + 0.2 * torch.randn(K), 0.1 * torch.randn(K)
+    wf, bf, sf = fold_layernorm(W, b, gamma, beta)
+    st = torch.empty(M, K // 64, 2, device=dev())
+    N.row_stats64(x, st)
+    out = torch.empty(M, Nn, device=dev(), dtype=torch.bfloat16)
+    N.gemm(x, wf.to(dev()), out, M, Nn, K, bias=bf.to(dev()), act=act, ln_stats=st, ln_colsum=sf.to(dev()),
+           ln_eps=1e-12)
+    ln = F.layer_norm(x.double(), (K,), gamma.double().to(dev()), beta.double().to(dev()), 1e-12)
+    ref = ln @ W.double().to(dev()).t() + b.double().to(dev())
+    ref = F.gelu(ref) if act == 2 else ref
+    # the sequence it replaces: LayerNorm kernel -> bf16 operand -> GEMM on W
+    a = torch.empty_like(x)
+    N.layernorm_fwd(x, gamma.to(dev()), beta.to(dev()), 1e-12, a)
+    seq = torch.empty_like(out)
+    N.gemm(a, W.to(dev(), torch.bfloat16), seq, M, Nn, K, bias=b.to(dev()), act=act)
+    e_fold, e_seq = _rel(out.double(), ref), _rel(seq.double(), ref)
+    print(f"LN fold rel-L2 {e_fold:.3e} vs LN->GEMM {e_seq:.3e}")
+    assert e_fold < 8e-3 and e_fold <= 1.1 * e_seq
+
+
+def test_gemm_stats_out_and_chain():
+    """A residual GEMM writes the per-64-column statistics of its bf16 output rows (stats_out); a
+    LayerNorm-folded GEMM reading them equals LN(out) W^T + b -- the encoder's o-proj -> fc1 chain."""
+    import torch.nn.functional as F
+    from encoder import fold_layernorm
+    torch.manual_seed(11)
+    M, E, F4 = 2000, 768, 3072
+    o = torch.randn(M, E, device=dev()).to(torch.bfloat16)
+    h = (3 * torch.randn(M, E, device=dev())).to(torch.bfloat16)
+    Wo = (torch.randn(E, E, device=dev()) / E ** 0.5).to(torch.bfloat16)
+    bo = 0.1 * torch.randn(E, device=dev())
+    st = torch.full((M, E // 64, 2), float("nan"), device=dev())
+    h2 = h.clone()
+    N.gemm(o, Wo, h2, M, E, E, bias=bo, residual=h2, stats_out=st)
+    ref_h = o.float() @ Wo.float().t() + bo + h.float()
+    assert _rel(h2, ref_h) < 5e-3
+    ref_st = _stats64_ref(h2)
+    assert (st.double() - ref_st).abs().max().item() <= 1e-4 * ref_st.abs().max().item()
+    W1 = torch.randn(F4, E) / E ** 0.5
+    b1, g, be = 0.1 * torch.randn(F4), 1 + 0.2 * torch.randn(E), 0.1 * torch.randn(E)
+    wf, bf, sf = fold_layernorm(W1, b1, g, be)
+    m = torch.empty(M, F4, device=dev(), dtype=torch.bfloat16)
+    N.gemm(h2, wf.to(dev()), m, M, F4, E, bias=bf.to(dev()), act=N.ACT_GELU, ln_stats=st, ln_colsum=sf.to(dev()),
+           ln_eps=1e-12)
+    ref = F.gelu(F.layer_norm(h2.double(), (E,), g.double().to(dev()), be.double().to(dev()), 1e-12)
+                 @ W1.double().to(dev()).t() + b1.double().to(dev()))
+    assert _rel(m.double(), ref) < 8e-3
+
+
+def test_gemm_layernorm_fold_rejects_bad_args():
+    x = torch.randn(256, 200, device=dev()).to(torch.bfloat16)
+    w = torch.randn(256, 200, device=dev()).to(torch.bfloat16)
+    out = torch.empty(256, 256, device=dev(), dtype=torch.bfloat16)
+    st = torch.zeros(256, 4, 2, device=dev())
+    with pytest.raises(N.NativeError, match="ln_stats"):  # K % 64 != 0
+        N.gemm(x, w, out, 256, 256, 200, ln_stats=st, ln_colsum=torch.zeros(256, device=dev()))
