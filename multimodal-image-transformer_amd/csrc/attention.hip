@@ -462,28 +462,11 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
 // Dropout (decoder cross-attention in training) is a template flag.
 // ------------------------------------------------------------------------------------------------
 constexpr int HK_MAX = 640;  // keys per head the LDS can hold (K + V = 256 B per key)
-// lazy-rescale threshold of attn_fwd_head in log2 units (0 = rescale every chunk, the default). 8
-// measured ViT-B/16 27.3 -> 27.0 us, CLIP-L/14@336 47.3 -> 44.4 us, the cfg1 step neutral (12603 vs
-// 12612 pairs/s interleaved, tools/gpu_ab.sh -m attn_bench.py, MIT_HIP_LIB), and it moved the cfg3 fixture's bf16 logits
-// error from 9.9e-3 to 1.03e-2, over the 1e-2 bound (rounding noise of P at another scale): off
-#ifndef MIT_ATTN_LAZY
-#define MIT_ATTN_LAZY 0
-#endif
-constexpr float LAZY_LOG2 = MIT_ATTN_LAZY;
-// diagnostic builds (wrong results): 1 = K/V staging only, 2 = no staging. ViT-B/16 MHSA: staging
-// alone 6.8-7.0 us (38.7 MB of K/V at ~5.6 TB/s), the sweep alone 22.2-22.4 us, both 26.9 us -- the
-// query sweep (VALU softmax + MFMA at 2 workgroups per CU), not the staging, bounds the kernel
-#ifndef MIT_ATTN_DIAG
-#define MIT_ATTN_DIAG 0
-#endif
-#ifndef MIT_ATTN_HS  // K/V staging: chunk rows per thread with their loads in flight together (4 vs 1,
-#define MIT_ATTN_HS 4  // tools/attn_bench.py: decoder cross 8.8 vs 9.4 us, ViT-B/16 and CLIP-L equal)
-#endif
-constexpr int HS = MIT_ATTN_HS;
-// query tiles per wave of the head-resident forward without dropout (attn_fwd_head2): compile-time A/B
-#ifndef MIT_ATTN_TP
-#define MIT_ATTN_TP 1
-#endif
+// K/V staging: chunk rows per thread with their loads in flight together (4 vs 1, tools/attn_bench.py:
+// decoder cross 8.8 vs 9.4 us, ViT-B/16 and CLIP-L equal). Measured and rejected: a lazy
+// softmax rescale (ViT-B/16 -0.3 us, CLIP-L -2.9 us, step neutral, but the cfg3 bf16 logits over the 1e-2
+// bound) and two 16-query tiles per wave (ViT-B/16 26.7 -> 30.6 us, decoder cross 8.8 -> 12.3 us).
+constexpr int HS = 4;
 
 // cross-lane reductions over the 4 lane groups of a 16-query tile (lanes l, l ^ 16, l ^ 32, l ^ 48
 // hold one query's key groups): v_permlane16_swap / v_permlane32_swap of a value with itself leave
@@ -524,7 +507,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
   // stage K and V: 8 16-B chunks per row, HS rows of chunks per thread with all their loads in flight
   // before the first LDS write (one round trip per HS, not per chunk row)
   const int nid = lkp * 8;
-  for (int base = tid; base < (MIT_ATTN_DIAG == 2 ? 0 : nid); base += HS * (int)blockDim.x) {
+  for (int base = tid; base < nid; base += HS * (int)blockDim.x) {
     u32x4 kv[HS], vv[HS];
 #pragma unroll
     for (int u = 0; u < HS; ++u) {
@@ -545,7 +528,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
     }
   }
   __syncthreads();
-  if (MIT_ATTN_DIAG == 1) return;  // diagnostic builds only (wrong results): staging alone
 
   const float sl2 = a.scale * 1.4426950408889634f;  // scores in log2 units
   const uint64_t key = DROP ? site_key(a.seed, a.site) : 0ull;
@@ -620,12 +602,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
       // l ^ 32, l ^ 48) through v_permlane16/32_swap (VALU) instead of ds_bpermute round trips
       float tmax = max16(s);
       tmax = xmax_rows(tmax);
-      // lazy rescale (the kernel is VALU-bound): the running max m moves only when some row's chunk
-      // max exceeds it by more than LAZY_LOG2 (wave-uniform); otherwise p = 2^(s - m) <= 2^LAZY_LOG2,
-      // in range for bf16 P and the f32 sums, and l / O need no rescale. O = ot / l is unchanged.
-      const float cand = tmax * sl2;  // finite: >= 1 unmasked key per chunk
-      if (LAZY_LOG2 <= 0.f || __builtin_amdgcn_ballot_w64(cand > m + LAZY_LOG2) != 0ull) {
-        const float mnew = __builtin_fmaxf(m, cand);
+      {
+        const float mnew = __builtin_fmaxf(m, tmax * sl2);  // finite: >= 1 unmasked key per chunk
         const float alpha = __builtin_amdgcn_exp2f(m - mnew);
         l *= alpha;
         lacc *= alpha;
@@ -742,219 +720,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
         *(bf16x4*)(O + i * 16 + g * 4) = o4;
       }
       if (a.lse && g == 0) a.lse[(b * H + h) * Lq + qi] = (m + __log2f(l)) * 0.6931471805599453f;
-    }
-  }
-}
-
-// attn_fwd_head with TWO 16-query tiles per wave (no dropout: the encoder MHSA and the decoder's cross-
-// attention in eval): both tiles' S^T MFMAs read the same K fragments, both P V^T products the same V
-// fragments, and one tile's softmax VALU has the other tile's MFMAs to hide under -- the one-tile kernel
-// is dependency-latency bound at ~3.5 waves per SIMD (~1000 SIMD-cycles per chunk
-// against ~530 of issue). Same per-element arithmetic as attn_fwd_head<false>.
-__global__ __attribute__((amdgpu_flat_work_group_size(64, 512), amdgpu_waves_per_eu(3))) void attn_fwd_head2(long H, long Lq, long Lk, AttnK a,
-                                                                                     int kbytes, int vbytes, int lkp) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* Ks = lds;
-  char* Vs = lds + (long)lkp * 128;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, nw = blockDim.x >> 6;
-  const long h = blockIdx.x, b = blockIdx.y;
-  MIT_DASSERT(h < H && Lk <= lkp && lkp <= HK_MAX && Lq > 0);
-  const bf16* Kb = (const bf16*)a.k + b * a.k_batch + h * D;
-  const bf16* Vb = (const bf16*)a.v + b * a.v_batch + h * D;
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)Kb, (short)0, kbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)Vb, (short)0, vbytes, 0x00020000);
-  const int nid = lkp * 8;
-  for (int base = tid; base < nid; base += HS * (int)blockDim.x) {
-    u32x4 kv[HS], vv[HS];
-#pragma unroll
-    for (int u = 0; u < HS; ++u) {
-      const int id = base + u * (int)blockDim.x, r = id >> 3, c = id & 7;
-      const bool ok = r < Lk;
-      kv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rk, (int)(ok ? (uint32_t)((r * a.k_row + c * 8) * 2) : A_OOB), 0, 0));
-      vv[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rv, (int)(ok ? (uint32_t)((r * a.v_row + c * 8) * 2) : A_OOB), 0, 0));
-    }
-#pragma unroll
-    for (int u = 0; u < HS; ++u) {
-      const int id = base + u * (int)blockDim.x, r = id >> 3, c = id & 7;
-      if (id < nid) {
-        *(u32x4*)(Ks + koff_k(r, c)) = kv[u];
-        *(u32x4*)(Vs + koff_v(r, c * 16)) = vv[u];
-      }
-    }
-  }
-  __syncthreads();
-
-  const float sl2 = a.scale * 1.4426950408889634f;
-  const int nqt = (int)((Lq + 15) / 16);
-  const int q = (lane & 15) >> 2, pp = lane & 3;
-  const int kofs = koff_k(lane & 15, g);
-  const int kofs1 = koff_k(lane & 15, 4 + g);
-  int vofs[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int colb = (i * 16 + 4 * pp) * 2;
-    vofs[i][0] = koff_v(g * 4 + q, colb);
-    vofs[i][1] = koff_v(16 + g * 4 + q, colb);
-  }
-  // wave w: tiles 2w and 2w + 1 (the second may not exist: wave-uniform, its work is done and dropped)
-  for (int qt0 = 2 * w; qt0 < nqt; qt0 += 2 * nw) {
-    bf16x8 qf[2][2];
-    long qi[2];
-    bool qlive[2];
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-      qi[T] = (long)(qt0 + T) * 16 + (lane & 15);
-      qlive[T] = qi[T] < Lq;
-      const bf16* Qr = (const bf16*)a.q + b * a.q_batch + h * D + (qlive[T] ? qi[T] : 0) * a.q_row;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        u32x4 v = *(const u32x4*)(Qr + kk * 32 + g * 8);
-        if (!qlive[T]) v = u32x4{0u, 0u, 0u, 0u};
-        qf[T][kk] = __builtin_bit_cast(bf16x8, v);
-      }
-    }
-    f32x4 ot[2][4];
-#pragma unroll
-    for (int T = 0; T < 2; ++T)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ot[T][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-    f32x4 lacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    const char* Kc = Ks;
-    const char* Vc = Vs;
-    int j0 = 0;
-    for (; j0 + 64 <= lkp; j0 += 64, Kc += 64 * 128, Vc += 64 * 128) {
-      f32x4 st[2][4];
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const bf16x8 k0 = __builtin_bit_cast(bf16x8, *(const u32x4*)(Kc + nb * 2048 + kofs));
-        const bf16x8 k1 = __builtin_bit_cast(bf16x8, *(const u32x4*)(Kc + nb * 2048 + kofs1));
-#pragma unroll
-        for (int T = 0; T < 2; ++T) {
-          st[T][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[T][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          st[T][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[T][1], st[T][nb], 0, 0, 0);
-        }
-      }
-      // softmax of both tiles (P packed to bf16 per 32-key half), then P V^T with each V fragment read once
-      // for both tiles (8 registers at a time instead of all 32)
-      bf16x8 pb[2][2];
-#pragma unroll
-      for (int T = 0; T < 2; ++T) {
-        float s[16];
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-          for (int t = 0; t < 4; ++t) s[nb * 4 + t] = st[T][nb][t];
-        if (j0 + 64 > Lk) {
-#pragma unroll
-          for (int k = 0; k < 16; ++k)
-            if (j0 + (k >> 2) * 16 + g * 4 + (k & 3) >= Lk) s[k] = -INFINITY;
-        }
-        const float tmax = xmax_rows(max16(s));
-        const float mnew = __builtin_fmaxf(m[T], tmax * sl2);
-        const float alpha = __builtin_amdgcn_exp2f(m[T] - mnew);
-        lacc[T] *= alpha;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ot[T][i] *= alpha;
-        m[T] = mnew;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pb[T][hh][j] = (bf16)__builtin_amdgcn_exp2f(fmaf(s[hh * 8 + j], sl2, -mnew));
-      }
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + hh * 4096 + vofs[i][0]));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + hh * 4096 + vofs[i][1]));
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-#pragma unroll
-          for (int T = 0; T < 2; ++T) ot[T][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[T][hh], ot[T][i], 0, 0, 0);
-        }
-#pragma unroll
-        for (int T = 0; T < 2; ++T) lacc[T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones8, pb[T][hh], lacc[T], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int T = 0; T < 2; ++T) l[T] = lacc[T][0];
-    const int ntail = (lkp - j0) >> 4;  // wave-uniform
-    if (ntail) {
-#pragma unroll
-      for (int T = 0; T < 2; ++T) {
-        f32x4 st[3];
-        float s[12];
-#pragma unroll
-        for (int nb = 0; nb < 3; ++nb) {
-          if (nb < ntail) {
-            const u32x4 k0 = *(const u32x4*)(Kc + nb * 2048 + kofs);
-            const u32x4 k1 = *(const u32x4*)(Kc + nb * 2048 + kofs1);
-            st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k0), qf[T][0],
-                                                              f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, k1), qf[T][1], st[nb], 0, 0, 0);
-          }
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            s[nb * 4 + t] = (nb < ntail && j0 + nb * 16 + g * 4 + t < Lk) ? st[nb][t] : -INFINITY;
-        }
-        float tmax = s[0];
-#pragma unroll
-        for (int k = 1; k < 12; ++k) tmax = __builtin_fmaxf(tmax, s[k]);
-        tmax = xmax_rows(tmax);
-        const float mnew = __builtin_fmaxf(m[T], tmax * sl2);
-        const float alpha = __builtin_amdgcn_exp2f(m[T] - mnew);
-        float p[12], psum = 0.f;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-          p[k] = __builtin_amdgcn_exp2f(fmaf(s[k], sl2, -mnew));
-          psum += p[k];
-        }
-        l[T] = l[T] * alpha + xsum_rows(psum);
-        m[T] = mnew;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ot[T][i] *= alpha;
-        if (ntail >= 2) {
-          bf16x8 pb;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pb[j] = (bf16)p[j];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + vofs[i][0]));
-            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + vofs[i][1]));
-            const s16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            ot[T][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pb, ot[T][i], 0, 0, 0);
-          }
-        }
-        if (ntail & 1) {
-          const int tb = ntail - 1;
-          const int voff = tb == 2 ? 4096 : 0;
-          typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-          bf16x4 pq;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) pq[t] = (bf16)p[(tb == 2 ? 8 : 0) + t];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + voff + vofs[i][0]));
-            ot[T][i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(lo, __builtin_bit_cast(s16x4, pq), ot[T][i], 0, 0, 0);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int T = 0; T < 2; ++T) {
-      if (!qlive[T]) continue;
-      const float inv = 1.0f / l[T];
-      bf16* O = (bf16*)a.o + b * a.o_batch + qi[T] * a.o_row + h * D;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-        bf16x4 o4 = {(bf16)(ot[T][i][0] * inv), (bf16)(ot[T][i][1] * inv), (bf16)(ot[T][i][2] * inv),
-                     (bf16)(ot[T][i][3] * inv)};
-        *(bf16x4*)(O + i * 16 + g * 4) = o4;
-      }
-      if (a.lse && g == 0) a.lse[(b * H + h) * Lq + qi[T]] = (m[T] + __log2f(l[T])) * 0.6931471805599453f;
     }
   }
 }
@@ -1436,10 +1201,8 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
       const int lkp = (int)((Lk + pad - 1) / pad * pad);
       const int nqt = (int)((Lq + 15) / 16);
       const int maxw = (a.dropout || 2 * lkp * 256 <= 160 * 1024) ? 8 : 16;
-      const int tp = (MIT_ATTN_TP == 2 && !a.dropout) ? 2 : 1;  // query tiles per wave
-      const int units = (nqt + tp - 1) / tp;
-      const int rounds = (units + (tp == 2 ? 8 : maxw) - 1) / (tp == 2 ? 8 : maxw);  // attn_fwd_head2: <= 8 waves
-      const int nw = (units + rounds - 1) / rounds;
+      const int rounds = (nqt + maxw - 1) / maxw;
+      const int nw = (nqt + rounds - 1) / rounds;
       const int lds = lkp * 256;
       static bool attr = false;
       if (!attr) {
@@ -1447,13 +1210,10 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
                                   HK_MAX * 256);
         (void)hipFuncSetAttribute((const void*)attn_fwd_head<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   HK_MAX * 256);
-        (void)hipFuncSetAttribute((const void*)attn_fwd_head2, hipFuncAttributeMaxDynamicSharedMemorySize, HK_MAX * 256);
         attr = true;
       }
       dim3 hg((unsigned)H, (unsigned)B);
-      if (tp == 2)
-        hipLaunchKernelGGL(attn_fwd_head2, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
-      else if (a.dropout)
+      if (a.dropout)
         hipLaunchKernelGGL(attn_fwd_head<true>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
       else
         hipLaunchKernelGGL(attn_fwd_head<false>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);

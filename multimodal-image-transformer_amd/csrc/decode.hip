@@ -180,25 +180,29 @@ __global__ __launch_bounds__(512) void attn_decode_rows_kernel(const bf16* __res
   float m = kNegBig, l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   // the U keys of an iteration as ONE online-softmax block: the U scores are independent (dot products
   // and head reductions pipeline), one max / one rescale per block and one exp2 per key (was a dependent
-  // max -> 2 exp2 -> rescale chain per key); head reductions over the LPH lanes by DPP within the row
-  for (long j0 = (long)w * U; j0 < Lk; j0 += 8 * U) {
-    bf16x8 kr[U], vr[U];
-    bool ok[U];
+  // max -> 2 exp2 -> rescale chain per key); head reductions over the LPH lanes by DPP within the row.
+  // The next block's K / V rows are loaded before this block's math (two register buffers): one memory
+  // round trip per wave instead of one per block (the cross-attention's 197 keys: 4 blocks per wave).
+  // the key-padding tokens of a block are loaded with its K / V rows (vmcnt counts in order: a token
+  // load issued after the next block's prefetch would wait for that prefetch too)
+  auto load_blk = [&](long j0, bf16x8 (&kr)[U], bf16x8 (&vr)[U], int64_t (&tk)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long j = j0 + u;
-      ok[u] = j < Lk;
-      if (ok[u]) {
+      if (j < Lk) {
         kr[u] = *(const bf16x8*)(kb + j * k_row);
         vr[u] = *(const bf16x8*)(vb + j * v_row);
+        tk[u] = tb ? tb[j] : 0;
       } else {
         kr[u] = vr[u] = bf16x8{};
+        tk[u] = pad_idx;
       }
     }
-    if (tb) {
+  };
+  auto math_blk = [&](long j0, const bf16x8 (&kr)[U], const bf16x8 (&vr)[U], const int64_t (&tk)[U]) {
+    bool ok[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) ok[u] = ok[u] && tb[j0 + u] != pad_idx;
-    }
+    for (int u = 0; u < U; ++u) ok[u] = j0 + u < Lk && (!tb || tk[u] != pad_idx);
     float s[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -228,6 +232,20 @@ __global__ __launch_bounds__(512) void attn_decode_rows_kernel(const bf16* __res
       for (int i = 0; i < 8; ++i) acc[i] = fmaf(p, (float)vr[u][i], acc[i]);
     }
     m = mn;
+  };
+  bf16x8 ka[U], va[U], kb2[U], vb2[U];
+  int64_t ta[U], tb2[U];
+  long j0 = (long)w * U;
+  if (j0 < Lk) load_blk(j0, ka, va, ta);
+  while (j0 < Lk) {
+    const long j1 = j0 + 8 * U;
+    if (j1 < Lk) load_blk(j1, kb2, vb2, tb2);
+    math_blk(j0, ka, va, ta);
+    if (j1 >= Lk) break;
+    const long j2 = j1 + 8 * U;
+    if (j2 < Lk) load_blk(j2, ka, va, ta);
+    math_blk(j1, kb2, vb2, tb2);
+    j0 = j2;
   }
   float* mine = red[w][lane];
   mine[0] = m;

@@ -405,8 +405,10 @@ class TransformerDecoder:
 
     def run_forward(self, tokens: torch.Tensor, mem: torch.Tensor, mem_ld: int, S: int, A: _Acts,
                     seed: Optional[torch.Tensor], train: bool, logits_out: Optional[torch.Tensor] = None,
-                    drop_p: Optional[float] = None, mem_keys: Optional[torch.Tensor] = None):
+                    drop_p: Optional[float] = None, mem_keys: Optional[torch.Tensor] = None,
+                    tick: Optional[Callable[[], None]] = None):
         """tokens int64 [B,T] (device); mem: memory rows [B*S, d] with row stride mem_ld.
+        tick: called before each layer's launches (the train step issues other work there).
         train=True keeps every layer's activations for run_backward (A must be a train arena);
         drop_p defaults to the module's dropout in train mode and 0 otherwise.
         mem_keys: optional int64 [B, S], 0 where the memory key is padding (memory_padding_mask,
@@ -424,6 +426,8 @@ class TransformerDecoder:
                          site=EMB_SITE)
         xin = A.x0
         for l in range(L):
+            if tick is not None:
+                tick()
             j = l if train else 0
             xs = A.xs[l] if train else A.xs[l % 2]
             z, stt = A.z[j], A.st[j]
@@ -462,8 +466,8 @@ class TransformerDecoder:
                      seed: Optional[torch.Tensor], dlogits: torch.Tensor,
                      proj_input: Optional[Tuple[torch.Tensor, int, int]] = None,
                      grads_ready: Optional[Callable[[str, str], None]] = None,
-                     mem_keys: Optional[torch.Tensor] = None):
-        """Backward of run_forward(train=True) given dlogits [R, V] (compute dtype).
+                     mem_keys: Optional[torch.Tensor] = None, tick: Optional[Callable[[], None]] = None):
+        """Backward of run_forward(train=True) given dlogits [R, V] (compute dtype); tick as in run_forward.
         proj_input = (enc_rows, ld, E): encoder features feeding the projection (for dW_proj).
         grads_ready(first, last) is called as soon as the grads of a contiguous entry span are final."""
         B, T = tokens.shape
@@ -541,6 +545,8 @@ class TransformerDecoder:
                                        device=self.device)
             side.run(lambda: native.gemm_grouped([kv_prob], A.gws_kv), reads=(A.dkv,))
         for l in reversed(range(L)):
+            if tick is not None:
+                tick()
             pre = f"layers.{l}."
             base = 64 * l
             xs, z, stt = A.xs[l], A.z[l], A.st[l]

@@ -39,6 +39,10 @@ def _dtype_from_config(dtype):
     return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32}[dtype]
 
 
+# encoder chunks (VisionEncoder.forward_iter: patch embedding, layers, final LayerNorm) of the prefetched
+# next batch issued before the decoder's first launch (train step)
+ENC_LEAD = int(os.environ.get("MIT_AB_ENC_LEAD", "2"))
+
 class GraphedStep:
     """A captured train step. step(images, decoder_input_tokens, target_tokens) copies a batch into
     the static buffers (skip by passing nothing) and replays; returns the loss device scalar. The
@@ -191,11 +195,29 @@ class ImageToTextModel:
         enc = self.encoder.forward(images, rows="all", slot=slot)  # [B, N, E]
         return enc.reshape(B * N, E), E, N
 
+    def _encoder_rows_iter(self, images: torch.Tensor, slot: int = 0):
+        """_encoder_rows as a generator of launch chunks (VisionEncoder.forward_iter)."""
+        B = images.shape[0]
+        N, E = self.encoder.N, self.encoder.E
+        if self.memory_mode == "cls":
+            enc = yield from self.encoder.forward_iter(images, rows="cls", slot=slot)
+            return enc, N * E, 1
+        enc = yield from self.encoder.forward_iter(images, rows="all", slot=slot)
+        return enc.reshape(B * N, E), E, N
+
     def prefetch_encoder(self, images: torch.Tensor):
         """Start the frozen encoder's forward for the NEXT batch on a second stream; the next
         train_step(images) consumes it instead of recomputing. The encoder has no trainable state, so
         its output does not depend on the step in between: the result is identical, and its GEMMs
         fill the CUs the decoder's small kernels leave idle. Double-buffered arenas (slot 0/1)."""
+        for _ in self.prefetch_encoder_iter(images):
+            pass
+
+    def prefetch_encoder_iter(self, images: torch.Tensor):
+        """prefetch_encoder as a generator: each next() issues one launch chunk of the encoder forward
+        (the patch embedding, one layer, the final LayerNorm) on the encoder stream. The train step
+        interleaves the chunks with its decoder layers, so neither stream's launches wait behind the
+        other's on the host (launches issue in program order, ~3.6 us each from a replayed plan)."""
         if self._enc_stream is None:
             self._enc_stream = torch.cuda.Stream(device=self.device)
             self._enc_events = native.HipEvents(8)
@@ -210,8 +232,15 @@ class ImageToTextModel:
             native.HipEvents.wait(enc, self._slot_free.pool[slot])
         else:
             self._enc_events.wait_stream(enc, native.stream_ptr())
-        with torch.cuda.stream(self._enc_stream):
-            out = self._encoder_rows(images, slot)
+        it = self._encoder_rows_iter(images, slot)
+        while True:
+            with torch.cuda.stream(self._enc_stream):  # (never left entered across a yield)
+                try:
+                    next(it)
+                except StopIteration as e:
+                    out = e.value
+                    break
+            yield
         ev = self._enc_events.record(enc)
         self._prefetched = (images, slot, out, ev)
 
@@ -314,12 +343,18 @@ class ImageToTextModel:
         targets = target_tokens.to(self.device, torch.int64, non_blocking=True).contiguous()
         B, T = tokens.shape
         mem, mem_ld, S, enc_rows, enc_ld = self._encode_memory(images, refresh=False)
-        if next_images is not None:
-            self.prefetch_encoder(next_images)
+        pf = self.prefetch_encoder_iter(next_images) if next_images is not None else None
+
+        def tick(n=1):
+            for _ in range(n if pf is not None else 0):
+                next(pf, None)
+        # the next batch's encoder: ENC_LEAD chunks now, then one per decoder layer (forward and backward),
+        # the rest after the backward
+        tick(ENC_LEAD)
         dec = self.decoder
         A = dec.acts(B, T, S, True)
         native.step_inc(self.seed_t)
-        logits, _ = dec.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, True)
+        logits, _ = dec.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, True, tick=tick)
         native.zero(A.count)
         native.zero(A.loss_sum)
         native.count_targets(targets, self.decoder_pad_idx, A.count)
@@ -329,7 +364,8 @@ class ImageToTextModel:
                              V=dec.V, ld=dec.Vp)
         proj = (enc_rows, enc_ld, self.encoder_output_dim) if self.has_projection else None
         dec.run_backward(tokens, mem, mem_ld, S, A, self.seed_t, logits, proj_input=proj,
-                         grads_ready=dist.grads_ready if dist is not None else None)
+                         grads_ready=dist.grads_ready if dist is not None else None, tick=tick)
+        tick(1 << 30)
         if self._enc_stream is not None:  # this step's last reader of its encoder slot is issued
             if self._slot_free is None:
                 self._slot_free = native.HipEvents(2)

@@ -211,24 +211,27 @@ def test_gemm_layernorm_fold(M, Nn, K, act):
     assert e_fold < 8e-3 and e_fold <= 1.1 * e_seq
 
 
-def test_gemm_stats_out_and_chain():
+@pytest.mark.parametrize("M,E,F4", [(2000, 768, 3072), (300, 64, 256), (257, 192, 128)])
+def test_gemm_stats_out_and_chain(M, E, F4):
     """A residual GEMM writes the per-64-column statistics of its bf16 output rows (stats_out); a
-    LayerNorm-folded GEMM reading them equals LN(out) W^T + b -- the encoder's o-proj -> fc1 chain."""
+    LayerNorm-folded GEMM reading them equals LN(out) W^T + b -- the encoder's o-proj -> fc1 chain
+    (E = 64 / 192: output widths narrower than the 256-column tile, whose idle waves write nothing)."""
     import torch.nn.functional as F
     from encoder import fold_layernorm
     torch.manual_seed(11)
-    M, E, F4 = 2000, 768, 3072
     o = torch.randn(M, E, device=dev()).to(torch.bfloat16)
     h = (3 * torch.randn(M, E, device=dev())).to(torch.bfloat16)
     Wo = (torch.randn(E, E, device=dev()) / E ** 0.5).to(torch.bfloat16)
     bo = 0.1 * torch.randn(E, device=dev())
-    st = torch.full((M, E // 64, 2), float("nan"), device=dev())
+    st_buf = torch.full((M + 1, E // 64, 2), float("nan"), device=dev())
+    st = st_buf[:M]
     h2 = h.clone()
     N.gemm(o, Wo, h2, M, E, E, bias=bo, residual=h2, stats_out=st)
     ref_h = o.float() @ Wo.float().t() + bo + h.float()
     assert _rel(h2, ref_h) < 5e-3
     ref_st = _stats64_ref(h2)
     assert (st.double() - ref_st).abs().max().item() <= 1e-4 * ref_st.abs().max().item()
+    assert torch.isnan(st_buf[M]).all()  # nothing written past the last row's partials
     W1 = torch.randn(F4, E) / E ** 0.5
     b1, g, be = 0.1 * torch.randn(F4), 1 + 0.2 * torch.randn(E), 0.1 * torch.randn(E)
     wf, bf, sf = fold_layernorm(W1, b1, g, be)

@@ -4,9 +4,18 @@ flight, per-queue busy time, and per kernel family the time it ran ALONE (nothin
 the critical-path suspects). Usage: python tools/step_timeline.py kernel_trace.csv"""
 import collections
 import csv
+import re
 import sys
 
-from trace_step import short
+
+def short(n):
+    """Kernel family name: the function name and its template arguments, namespaces dropped."""
+    n = n.replace("(anonymous namespace)::", "")
+    if n.startswith("_ZN12_GLOBAL__N_1"):
+        m = re.match(r"_ZN12_GLOBAL__N_1\d+(\w+?)I(.*)E", n)
+        return (m.group(1) + "<" + m.group(2)[:40] + ">") if m else n[:60]
+    m = re.match(r"^(?:void )?(\w+)(<[^>]*>)?", n)
+    return (m.group(1) + (m.group(2) or "")) if m else n[:60]
 
 
 def main():
