@@ -328,6 +328,10 @@ int mit_greedy_pick(long B, long V, const float* logits, long ld, int64_t* ids, 
  * separate mit_step_inc launch folded in. */
 int mit_greedy_pick_advance(long B, long V, const float* logits, long ld, int64_t* ids, long ld_ids, int64_t* pos,
                             int64_t end_id, int64_t pad_id, int* finished, int* n_finished, int* ticket, void* stream);
+/* greedy_pick_advance from the argmax keys a mit_decode_gemm (argmax_keys) left: column
+ * 0xFFFFFFFF - (u32)keys[b] is row b's pick; the keys are reset to 0 and *pos advanced (one block). */
+int mit_greedy_pick_keys(long B, unsigned long long* keys, int64_t* ids, long ld_ids, int64_t* pos, int64_t end_id,
+                         int64_t pad_id, int* finished, int* n_finished, void* stream);
 
 /* Decode-step GEMM with the decoder's post-LN residual blocks folded in (bf16 only; the B-row GEMMs of
  * one token step, torch/nn/modules/transformer.py:1144-1153 norm_first=False):
@@ -367,6 +371,13 @@ typedef struct {
   void* cache;
   long c_row, c_batch, kv_col0;
   const int64_t* pos;
+  /* argmax_keys (u64 [M], NULL: off): the greedy pick folded into the vocabulary head. Each row's
+   * maximum over the N columns of act(A . B^T + bias) leaves as one atomic max of
+   * ord(value) << 32 | (0xFFFFFFFF - column) (ord: the order-preserving u32 image of an f32, NaN
+   * largest), so the surviving key is the first maximal column (torch.argmax). bf16 A rows, no residual
+   * or activation; C / z_out may be NULL. The keys must be 0 before the launch (mit_greedy_pick_keys
+   * leaves them 0). */
+  unsigned long long* argmax_keys;
 } mit_decode_gemm_args;
 int mit_decode_gemm(const mit_decode_gemm_args* args, void* stream);
 /* out[m, :] = LN(z[m, :]) (bf16) from the statistics a mit_decode_gemm stats_out wrote (W <= 1024):

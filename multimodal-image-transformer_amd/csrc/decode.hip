@@ -627,6 +627,25 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(mit_decode_gemm_ar
       v[c + i] = x + res[c + i];
     }
   }
+  if constexpr (RMODE == 3) {  // greedy pick folded in: the row's (value, first column) maximum of this tile
+    uint64_t best = 0;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const long gc = n0 + cq + c;
+      const uint32_t u = __float_as_uint(v[c]);
+      const uint32_t o = v[c] != v[c] ? 0xFFFFFFFFu : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
+      const uint64_t k = ((uint64_t)o << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)gc);
+      if (gc < N && k > best) best = k;
+    }
+#pragma unroll
+    for (int x = 1; x < TPR; x <<= 1) {
+      const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(best >> 32), x, 64) << 32) |
+                         (uint32_t)__shfl_xor((int)(uint32_t)best, x, 64);
+      best = o > best ? o : best;
+    }
+    if (rok && (tid % TPR) == 0) atomicMax(g.argmax_keys + gr, (unsigned long long)best);
+    return;
+  }
   if (g.stats_out) {  // this tile's (mean, M2) per row over its valid columns; TPR lanes per row
     const int nv = (int)min(64L, N - n0);
     float sm = 0.f;
@@ -808,6 +827,42 @@ extern "C" int mit_greedy_pick(long B, long V, const float* logits, long ld, int
   return MIT_OK;
 }
 
+// one block: row b's pick from the head's argmax key, the key reset, then *pos += 1 once every row has
+// read the old position (the __syncthreads orders the block's reads before thread 0's write)
+__global__ __launch_bounds__(1024) void greedy_pick_keys_kernel(long B, unsigned long long* __restrict__ keys,
+                                                                int64_t* __restrict__ ids, long ld_ids, int64_t* pos,
+                                                                int64_t end_id, int64_t pad_id, int* __restrict__ finished,
+                                                                int* __restrict__ n_finished) {
+  const long p = *pos;
+  for (long b = threadIdx.x; b < B; b += blockDim.x) {
+    const unsigned long long k = keys[b];
+    keys[b] = 0ull;
+    const int64_t bi = (int64_t)(0xFFFFFFFFu - (uint32_t)k);
+    if (finished[b]) {
+      ids[b * ld_ids + p + 1] = pad_id;
+    } else {
+      ids[b * ld_ids + p + 1] = bi;
+      if (bi == end_id) {
+        finished[b] = 1;
+        atomicAdd(n_finished, 1);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *pos = p + 1;
+}
+
+extern "C" int mit_greedy_pick_keys(long B, unsigned long long* keys, int64_t* ids, long ld_ids, int64_t* pos,
+                                    int64_t end_id, int64_t pad_id, int* finished, int* n_finished, void* stream) {
+  MIT_RECORD([=]() { return mit_greedy_pick_keys(B, keys, ids, ld_ids, pos, end_id, pad_id, finished, n_finished, stream); });
+  MIT_CHECK_ARG(keys && ids && pos && finished && n_finished, "mit_greedy_pick_keys: null pointer");
+  MIT_CHECK_ARG(B > 0 && B < (1L << 30), "mit_greedy_pick_keys: B = %ld", B);
+  hipLaunchKernelGGL(greedy_pick_keys_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, keys, ids, ld_ids, pos,
+                     end_id, pad_id, finished, n_finished);
+  MIT_LAUNCH_CHECK("mit_greedy_pick_keys");
+  return MIT_OK;
+}
+
 extern "C" int mit_greedy_pick_advance(long B, long V, const float* logits, long ld, int64_t* ids, long ld_ids,
                                        int64_t* pos, int64_t end_id, int64_t pad_id, int* finished, int* n_finished,
                                        int* ticket, void* stream) {
@@ -854,7 +909,7 @@ extern "C" int mit_decode_gemm(const mit_decode_gemm_args* g, void* stream) {
   MIT_RECORD([c = *g, stream]() { return mit_decode_gemm(&c, stream); });
   MIT_CHECK_ARG(g->M >= 0 && g->N > 0 && g->K > 0, "mit_decode_gemm: bad extents M=%ld N=%ld K=%ld", g->M, g->N, g->K);
   MIT_CHECK_ARG(g->A && g->B, "mit_decode_gemm: null operand");
-  MIT_CHECK_ARG(g->C || g->z_out, "mit_decode_gemm: no output");
+  MIT_CHECK_ARG(g->C || g->z_out || g->argmax_keys, "mit_decode_gemm: no output");
   MIT_CHECK_ARG(g->K % 8 == 0 && g->N % 8 == 0 && g->ldb % 8 == 0 && g->lda >= g->K && g->ldb >= g->K,
                 "mit_decode_gemm: K, N, ldb must be multiples of 8 and lda/ldb >= K");
   MIT_CHECK_ARG(g->act == MIT_ACT_NONE || g->act == MIT_ACT_RELU, "mit_decode_gemm: act %d unsupported", g->act);
@@ -877,8 +932,12 @@ extern "C" int mit_decode_gemm(const mit_decode_gemm_args* g, void* stream) {
                        (uintptr_t)g->cache | (uintptr_t)g->a_gamma | (uintptr_t)g->a_beta | (uintptr_t)g->r_gamma |
                        (uintptr_t)g->r_beta;
   MIT_CHECK_ARG(al % 16 == 0, "mit_decode_gemm: pointers must be 16-B aligned");
+  MIT_CHECK_ARG(!g->argmax_keys || (!lna && g->act == MIT_ACT_NONE && g->r_mode == 0 && !g->C && !g->z_out &&
+                                     !g->cache && ((uintptr_t)g->argmax_keys % 8) == 0 && g->N < (1L << 32)),
+                "mit_decode_gemm: argmax_keys needs bf16 A rows, no activation / residual / other output");
   if (g->M == 0) return MIT_OK;
   hipStream_t s = (hipStream_t)stream;
+  if (g->argmax_keys) return launch_decode_gemm<0, MIT_ACT_NONE, 3, false>(g, s);
   const bool relu = g->act == MIT_ACT_RELU;
   if (g->c_f32) {
     MIT_CHECK_ARG(lna && !relu && g->r_mode == 0, "mit_decode_gemm: f32 C only for the LN-operand head GEMM");

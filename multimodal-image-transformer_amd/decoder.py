@@ -284,6 +284,7 @@ class DecodeState:
             self.z = [torch.empty(B, d, dtype=torch.float32, device=dev) for _ in range(3)]
             self.zst = [torch.empty(B, P, 2, dtype=torch.float32, device=dev) for _ in range(3)]
             self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.keys = torch.zeros(B, dtype=torch.int64, device=dev)  # the head's packed argmax (0 between steps)
 
     def token_lists(self) -> List[List[int]]:
         """Per row: START .. up to and including the first END (model.py:236-242), else max_len ids."""
@@ -751,7 +752,8 @@ class TransformerDecoder:
         block (transformer.py:1144-1153) is z = sublayer + LN_prev(z_prev) written in f32 by the
         GEMM that produces the sublayer output, and LN(z) is applied by its consumers (the next
         GEMM's operand staging / residual epilogue); the self-attention K|V row goes straight from the
-        in_proj GEMM into the cache; the pick advances the position."""
+        in_proj GEMM into the cache; the vocabulary head leaves each row's argmax as a packed atomic max
+        (no logits in HBM) and the pick reads it and advances the position."""
         d, H, L, V = self.d, self.H, self.L, self.V
         st, w, p = self.store, self.store.w, self.store.p
         B, S, Tm = stt.B, stt.S, stt.max_len
@@ -788,9 +790,8 @@ class TransformerDecoder:
                                z_out=z3, stats_out=s3)
         q3 = f"layers.{L - 1}.norm3."
         native.decode_layernorm(z3, s3, p(q3 + "weight"), p(q3 + "bias"), stt.x)
-        native.linear(stt.x, w("fc_out.weight"), stt.logits, bias=p("fc_out.bias"))
-        native.greedy_pick_advance(stt.logits, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished,
-                                   stt.n_finished, stt.ticket, V=V)
+        native.decode_gemm(stt.x, w("fc_out.weight")[:V], bias=p("fc_out.bias")[:V], argmax_keys=stt.keys)
+        native.greedy_pick_keys(stt.keys, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished, stt.n_finished)
 
     def forward_ops(self, tokens: torch.Tensor, mem: torch.Tensor, S: int, params: Dict[str, torch.Tensor],
                     seed: Optional[torch.Tensor], drop_p: float, mem_keys: Optional[torch.Tensor] = None) -> torch.Tensor:

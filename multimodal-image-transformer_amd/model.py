@@ -346,8 +346,11 @@ class ImageToTextModel:
         pf = self.prefetch_encoder_iter(next_images) if next_images is not None else None
 
         def tick(n=1):
-            for _ in range(n if pf is not None else 0):
-                next(pf, None)
+            nonlocal pf
+            while pf is not None and n > 0:
+                if next(pf, tick) is tick:  # exhausted: the prefetch is fully issued
+                    pf = None
+                n -= 1
         # the next batch's encoder: ENC_LEAD chunks now, then one per decoder layer (forward and backward),
         # the rest after the backward
         tick(ENC_LEAD)

@@ -18,7 +18,7 @@ from torch.utils._python_dispatch import TorchDispatchMode
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MIT_HIP_LIB", os.path.join(_HERE, "lib", "libmit_hip.so"))
-ABI_VERSION = 3  # mit_abi_version() of the library this binding matches (include/mit_hip.h)
+ABI_VERSION = 4  # mit_abi_version() of the library this binding matches (include/mit_hip.h)
 
 F32, BF16 = 0, 1
 K_CONTIG, MN_CONTIG = 0, 1
@@ -52,7 +52,7 @@ class DecodeGemmArgs(ctypes.Structure):
                 ("a_beta", vp), ("B", vp), ("ldb", L), ("bias", vp), ("act", I), ("c_f32", I), ("C", vp),
                 ("ldc", L), ("r_mode", I), ("r", vp), ("ldr", L), ("r_stats", vp), ("r_gamma", vp),
                 ("r_beta", vp), ("eps", Fl), ("z_out", vp), ("ldz", L), ("stats_out", vp), ("cache", vp),
-                ("c_row", L), ("c_batch", L), ("kv_col0", L), ("pos", vp)]
+                ("c_row", L), ("c_batch", L), ("kv_col0", L), ("pos", vp), ("argmax_keys", vp)]
 
 
 class LnGradsJob(ctypes.Structure):
@@ -123,6 +123,7 @@ SIGNATURES = {
     "mit_stream_wait_event": (I, [vp, vp]),
     "mit_greedy_pick": (I, [L, L, vp, L, vp, L, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp]),
     "mit_greedy_pick_advance": (I, [L, L, vp, L, vp, L, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp]),
+    "mit_greedy_pick_keys": (I, [L, vp, vp, L, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp]),
     "mit_decode_gemm": (I, [ctypes.POINTER(DecodeGemmArgs), vp]),
     "mit_decode_layernorm": (I, [L, L, vp, L, vp, vp, vp, Fl, vp, L, vp]),
 }
@@ -736,12 +737,14 @@ def greedy_pick_advance(logits, ids, pos, end_id, pad_id, finished, n_finished, 
 
 
 def decode_gemm(a, w, *, out=None, bias=None, act=ACT_NONE, a_ln=None, residual=None, r_ln=None, eps=1e-5,
-                z_out=None, stats_out=None, cache=None, c_row=0, c_batch=0, kv_col0=0, pos=None):
+                z_out=None, stats_out=None, cache=None, c_row=0, c_batch=0, kv_col0=0, pos=None, argmax_keys=None):
     """Decode-step GEMM (mit_decode_gemm): out = act(A' w^T + bias) (+ residual), w bf16 [N, K].
     a: bf16 rows [M, K], or f32 pre-LN sums when a_ln = (stats, gamma, beta) (A' = LN(a));
     residual: bf16 rows, or f32 pre-LN sums when r_ln = (stats, gamma, beta) (+ LN(residual));
     z_out / stats_out: f32 pre-LN sum of the next LayerNorm and its per-64-column row statistics
-    [M, ceil(N/64), 2]; cache: the columns >= kv_col0 also go to cache[m*c_batch + pos*c_row + n - kv_col0]."""
+    [M, ceil(N/64), 2]; cache: the columns >= kv_col0 also go to cache[m*c_batch + pos*c_row + n - kv_col0];
+    argmax_keys: int64 [M] zeros <- each row's packed (value, first column) maximum (the greedy pick
+    folded into the head: greedy_pick_keys)."""
     M, K = a.shape[0], a.shape[-1]
     N = w.shape[0]
     r_mode = 0 if residual is None else (2 if r_ln is not None else 1)
@@ -752,8 +755,15 @@ def decode_gemm(a, w, *, out=None, bias=None, act=ACT_NONE, a_ln=None, residual=
                        residual.stride(0) if residual is not None else 0, ptr(r_ln[0]) if r_ln else None,
                        ptr(r_ln[1]) if r_ln else None, ptr(r_ln[2]) if r_ln else None, eps, ptr(z_out),
                        z_out.stride(0) if z_out is not None else 0, ptr(stats_out), ptr(cache), c_row, c_batch, kv_col0,
-                       ptr(pos))
+                       ptr(pos), ptr(argmax_keys))
     _check(lib().mit_decode_gemm(ctypes.byref(g), stream_ptr()), "mit_decode_gemm")
+
+
+def greedy_pick_keys(keys, ids, pos, end_id, pad_id, finished, n_finished):
+    """ids[:, pos + 1] <- the picks a decode_gemm(argmax_keys=keys) left (keys reset to 0), then pos += 1."""
+    B = keys.shape[0]
+    _check(lib().mit_greedy_pick_keys(B, ptr(keys), ptr(ids), ids.shape[1], ptr(pos), int(end_id), int(pad_id),
+                                      ptr(finished), ptr(n_finished), stream_ptr()), "mit_greedy_pick_keys")
 
 
 def decode_layernorm(z, stats, gamma, beta, out, eps=1e-5):

@@ -454,6 +454,30 @@ def test_gemm_grouped_weight_gradients_match_single_launches(R):
         assert torch.allclose(C, C1, rtol=1e-5, atol=1e-3) and torch.allclose(rs, rs1, rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("M,Nn,K,layout", [(4032, 512, 2048, "nt"), (4032, 512, 1536, "nn"), (520, 512, 2048, "nn")])
+def test_gemm_split_k_bias_residual(M, Nn, K, layout):
+    """The decoder's long-K N = 512 GEMMs (fc2 forward: bias; the fc1 / self_in data gradients: a residual
+    accumulated in place) run split-K when given a workspace, the reduce applying bias and residual:
+    equal to float64 torch, and to the same GEMM without a workspace (one launch, no split)."""
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(K + M)
+    A = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    bl = N.K_CONTIG if layout == "nt" else N.MN_CONTIG
+    B = (torch.randn(Nn, K, generator=g) if layout == "nt" else torch.randn(K, Nn, generator=g)).to(dev, torch.bfloat16)
+    bias = torch.randn(Nn, generator=g).to(dev)
+    R0 = torch.randn(M, Nn, generator=g).to(dev, torch.bfloat16)
+    Bt = B.double().cpu() if layout == "nt" else B.double().cpu().t()
+    ref = A.double().cpu() @ Bt.t() + bias.double().cpu() + R0.double().cpu()
+    ws = N.gemm_workspace(M, Nn, K, dev)
+    outs = []
+    for w in (ws, None):
+        C = R0.clone()  # residual aliases the output (dx += ...)
+        N.gemm(A, B, C, M, Nn, K, b_layout=bl, bias=bias, residual=C, workspace=w)
+        outs.append(C)
+        assert (C.double().cpu() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    assert ((outs[0].float() - outs[1].float()).norm() / outs[1].float().norm()).item() < 5e-3
+
+
 def test_gemm_grouped_rejects_unsupported():
     dev = torch.device("cuda")
     A = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
