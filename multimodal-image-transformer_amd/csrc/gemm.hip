@@ -1394,22 +1394,15 @@ __global__ __launch_bounds__(256) void gemm_rs_kernel(const bf16* __restrict__ A
 }
 
 // C = alpha * sum_s slab[s] (f32 or bf16 out, optional accumulate); rowsum = sum_s rowslab[s]
-// C = alpha * (sum of the K-slice slabs) + bias (+ residual): the epilogue of a split GEMM without an
-// activation, in the single-launch epilogue's order (residual bf16, may alias C)
 __global__ void gemm_splitk_reduce(long M, long N, int ksplit, const float* __restrict__ ws, void* C, long ldc,
-                                   float alpha, int out_f32, int accumulate, float* rowsum, const float* bias,
-                                   const bf16* res, long ldr) {
+                                   float alpha, int out_f32, int accumulate, float* rowsum) {
   typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
   const long n4 = N / 4, total = M * n4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const long r = i / n4, c = (i % n4) * 4;
-    const f32x4 b = bias ? *(const f32x4*)(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x4 x = {};
-    if (res) x = *(const bf16x4*)(res + r * ldr + c);
     f32x4 s = *(const f32x4*)(ws + r * N + c);
     for (int k = 1; k < ksplit; ++k) s += *(const f32x4*)(ws + ((long)k * M + r) * N + c);
-    s = s * alpha + b;
-    if (res) s += f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+    s *= alpha;
     if (out_f32) {
       f32x4* o = (f32x4*)((float*)C + r * ldc + c);
       if (accumulate) s += *o;
@@ -1760,16 +1753,12 @@ Split plan_split(const mit_gemm_args* g) {
   Split p;
   p.kchunk = g->K;
   if (!g->workspace || !al16(g->workspace)) return p;
-  // epilogues the reduce applies: alpha, bias, a bf16 residual (the decoder's fc2 forward and its
-  // residual-accumulating data gradients, K = 1536 / 2048 on 128 tiles)
-#ifndef MIT_SPLIT_EPI
-#define MIT_SPLIT_EPI 1
-#endif
-  const bool reducible = g->act == MIT_ACT_NONE && !g->aux && g->drop_p <= 0.f && (!g->bias || al16(g->bias)) &&
-                         (!g->residual || (g->ldr % 4 == 0 && ((uintptr_t)g->residual % 8) == 0 && !g->accumulate)) &&
-                         (MIT_SPLIT_EPI || (!g->bias && !g->residual));
+  // plain epilogues only: splitting the decoder's long-K GEMMs that carry a bias / residual (fc2 forward,
+  // the fc1 / self_in data gradients; the reduce applying them) cost 1.8 % of the step (12639 / 12702 vs
+  // 12885 / 12898 pairs/s): their extra workgroups and reduce launches take CUs from the encoder prefetch
+  const bool plain = !g->bias && g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f;
   long kc;
-  if (reducible && g->ldc % 4 == 0 && al16(g->C)) {
+  if (plain && g->ldc % 4 == 0 && al16(g->C)) {
     const int s = splitk_plan(g->M, g->N, g->K, &kc, g->a_layout);
     if (s > 1 && splitk_ws_bytes(g->M, g->N, s) <= g->workspace_bytes) {
       p.ks = s;
@@ -1892,7 +1881,7 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
       if (blocks > 4096) blocks = 4096;
       hipLaunchKernelGGL(gemm_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, g->M, g->N, sp.ks,
                          (const float*)((char*)g->workspace + WS_HDR), g->C, g->ldc, g->alpha, g->out_f32,
-                         g->accumulate, g->rowsum, g->bias, (const bf16*)g->residual, g->ldr);
+                         g->accumulate, g->rowsum);
     }
   } else {
     if (g->a_layout == 0 && g->b_layout == 0) launch_f32<0, 0>(g, e, s);

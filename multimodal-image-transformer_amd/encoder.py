@@ -17,7 +17,6 @@ Also the counterpart of the reference's standalone encoder.py helpers (encoder.p
 from __future__ import annotations
 
 import math
-import os
 import re
 from typing import Dict, Optional
 
@@ -87,8 +86,7 @@ class VisionEncoder:
         # towers only: on the 2-layer CLIP-336 cls fixture the folded path's largest logit error (0.039) left
         # the asserted 1.5x of the reference's own bf16 error (0.037) while its encoder rel-L2 improved
         # (5.40e-3 vs 5.54e-3); the deep CLIP-L towers run the f32 residual stream anyway
-        self.fold_ln = (dtype == torch.bfloat16 and not self.res32 and self.E % 64 == 0 and self.kind == "vit"
-                        and os.environ.get("MIT_AB_NOFOLD") != "1")
+        self.fold_ln = dtype == torch.bfloat16 and not self.res32 and self.E % 64 == 0 and self.kind == "vit"
         self.w: Dict[str, torch.Tensor] = {}
         self._ws = {}
 

@@ -457,8 +457,8 @@ def test_gemm_grouped_weight_gradients_match_single_launches(R):
 @pytest.mark.parametrize("M,Nn,K,layout", [(4032, 512, 2048, "nt"), (4032, 512, 1536, "nn"), (520, 512, 2048, "nn")])
 def test_gemm_split_k_bias_residual(M, Nn, K, layout):
     """The decoder's long-K N = 512 GEMMs (fc2 forward: bias; the fc1 / self_in data gradients: a residual
-    accumulated in place) run split-K when given a workspace, the reduce applying bias and residual:
-    equal to float64 torch, and to the same GEMM without a workspace (one launch, no split)."""
+    accumulated in place, output aliasing it) against float64 torch, with and without a split-K workspace
+    (a bias / residual epilogue keeps them in one launch: DESIGN.md §4.1f)."""
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(K + M)
     A = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)

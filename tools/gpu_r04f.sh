@@ -11,3 +11,5 @@ for r in 1 2 3; do
   echo "## nosplit $(MIT_LIB=$V timeout -k 10 200 python -u bench.py $B | cut -c90-150)"
 done
 timeout -k 10 200 python -u bench.py $B > gpurun_out/r04f/bench.json 2>&1
+timeout -k 10 200 python -u tools/step_parts.py
+MIT_LIB=$V timeout -k 10 200 python -u tools/step_parts.py
