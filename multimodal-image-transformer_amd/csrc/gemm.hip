@@ -694,6 +694,8 @@ constexpr int HALF_BYTES = 128 * 64 * 2;  // one 128-row x BK half-tile
 constexpr int BUF_BYTES = 4 * HALF_BYTES;
 constexpr int EPI_LD = 68;                // per-wave fp32 epilogue stage [64][68]
 constexpr int SMEM2_BYTES = (2 * BUF_BYTES > 8 * 64 * EPI_LD * 4) ? 2 * BUF_BYTES : 8 * 64 * EPI_LD * 4;
+constexpr int LN_PMAX = 16;                                 // LN fold: statistics partials per row (K <= 1024)
+constexpr int SMEM2_LN_BYTES = SMEM2_BYTES + 256 * 8;       // + the tile's per-row (rstd, -rstd mean)
 
 // Per-lane LDS-DMA source plan for one operand (8 waves x 2 wave-instructions per half-tile):
 // byte offsets of this lane's two 16-B chunks in each half at K-tile 0 (OOB when the row / column
@@ -817,28 +819,6 @@ __device__ __forceinline__ void reg_epilogue(const f32x4 (&acc)[MI][4], const Ep
 // 5.9 -> 4.8 us; enc qkv+bias 51.1 -> 48.8 us, fc1 73.8 -> 68.8, kv_all 102 -> 94.7; residual loads as
 // 8-B segments in the accumulator layout instead: slower (o+res 28.6 -> 31.9 us). Image: row r at
 // r * 128 B, 16-B chunk c at (c ^ (r & 7)) * 16 (the 8-row x 8-chunk read-back is conflict-free).
-// Chan merge of two (count, mean, M2) row aggregates in a fixed order (a, then b): every lane that
-// merges the same pair gets the same bits
-__device__ __forceinline__ void chan_merge(float& n, float& m, float& q, float na, float ma, float qa, float nb, float mb,
-                                           float qb) {
-  const float nt = na + nb, d = mb - ma, f = nt > 0.f ? nb / nt : 0.f;
-  n = nt;
-  m = ma + d * f;
-  q = qa + qb + d * d * na * f;
-}
-// (count, mean, M2) over the 4 lane groups of a row (lanes l, l^16, l^32, l^48): v_permlane16_swap /
-// v_permlane32_swap of a value with itself return the pair's lower-group value first, so both lanes of a
-// pair merge in the same order
-__device__ __forceinline__ void chan_merge_rows(float& n, float& m, float& q) {
-  auto sw16 = [](float x) { return __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false); };
-  auto sw32 = [](float x) { return __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false); };
-  const auto a = sw16(n), b = sw16(m), c = sw16(q);
-  chan_merge(n, m, q, __uint_as_float(a[0]), __uint_as_float(b[0]), __uint_as_float(c[0]), __uint_as_float(a[1]),
-             __uint_as_float(b[1]), __uint_as_float(c[1]));
-  const auto a2 = sw32(n), b2 = sw32(m), c2 = sw32(q);
-  chan_merge(n, m, q, __uint_as_float(a2[0]), __uint_as_float(b2[0]), __uint_as_float(c2[0]), __uint_as_float(a2[1]),
-             __uint_as_float(b2[1]), __uint_as_float(c2[1]));
-}
 __device__ __forceinline__ float sum_rows(float v) {
   const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
@@ -846,13 +826,14 @@ __device__ __forceinline__ float sum_rows(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-// LNX: 0 = plain; 1 = LayerNorm-folded operand (the wave's rows' (mean, rstd) merged from e.ln_stats:
-// lane group g takes partials g, g+4, g+8, g+12, then chan_merge_rows; v = rstd (acc - mean colsum) +
-// bias); 2 = also write the per-64-column (mean, M2) of the bf16-rounded output rows to e.stats_out
-// (the next LayerNorm's statistics: this wave's 64 columns are one partial)
+// LNX: 0 = plain; 1 = LayerNorm-folded operand (v = rstd (acc - mean colsum) + bias, with the wave's rows'
+// (rstd, -rstd mean) from lnrow: merged once per tile row in the kernel's prologue, ln_rows); 2 = also
+// write the per-64-column (mean, M2) of the bf16-rounded output rows to e.stats_out (the next LayerNorm's
+// statistics: this wave's 64 columns are one partial)
 template <int ACT, bool DROP, bool XOPS, int LNX = 0>
 __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const Epi& e, void* C, long ldc, long M,
-                                               long N, long mw, long nw, int lane, char* stg) {
+                                               long N, long mw, long nw, int lane, char* stg,
+                                               const f32x2* lnrow = nullptr) {
   constexpr int PASSES = 1, IP = 8;  // one pass over the wave's 8 16-row blocks
   const int g = lane >> 4, r16 = lane & 15;
   float bj[4][4];
@@ -867,22 +848,12 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
     }
   }
   float sj[LNX == 1 ? 4 : 1][4];  // LN fold: the column sums of the folded weight rows
-  f32x2 lp[LNX == 1 ? 8 : 1][4];  // LN fold: this lane's statistics partials of its 8 rows
   if constexpr (LNX == 1) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long c = nw + 16 * j + 4 * g;
       const f32x4 b = c < N ? *(const f32x4*)(e.ln_colsum + c) : f32x4{0.f, 0.f, 0.f, 0.f};
       sj[j][0] = b[0]; sj[j][1] = b[1]; sj[j][2] = b[2]; sj[j][3] = b[3];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const long row = mw + 16 * i + r16;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int pi = g + 4 * u;
-        lp[i][u] = (row < M && pi < e.ln_parts) ? *(const f32x2*)(e.ln_stats + (row * e.ln_parts + pi) * 2) : f32x2{0.f, 0.f};
-      }
     }
   }
   typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
@@ -906,25 +877,9 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
   if constexpr (LNX == 1) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float s = 0.f, cnt = 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (g + 4 * u < e.ln_parts) {
-          s += lp[i][u][0];
-          cnt += 1.f;
-        }
-      float m = cnt > 0.f ? s / cnt : 0.f, q = 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (g + 4 * u < e.ln_parts) {
-          const float d = lp[i][u][0] - m;
-          q += lp[i][u][1] + 64.f * d * d;
-        }
-      float n = 64.f * cnt;
-      chan_merge_rows(n, m, q);
-      const float rs = __builtin_amdgcn_rsqf(q / n + e.ln_eps);
-      rs_i[i] = rs;
-      nr_i[i] = -rs * m;
+      const f32x2 v = lnrow[16 * i + r16];
+      rs_i[i] = v[0];
+      nr_i[i] = v[1];
     }
   }
 #pragma unroll
@@ -1128,12 +1083,42 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
                     : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], acc[ih * IH0 + i][jh * 2 + j], 0, 0, 0);
   };
 
+  // LN fold (STG 3): each of the tile's 256 rows' K / 64 statistics partials merged ONCE here (thread r
+  // takes row m0 + r, Chan's rule in column order) into (rstd, -rstd mean) in LDS past the K-tile buffers,
+  // read by the epilogue's 8 rows per lane. The partial loads go out before the first LDS-DMA, so the
+  // K loop's counted vmcnt waits (younger DMAs only) stay exact, and the merge after the prologue's DMA
+  // issue waits for them alone; their round trip overlaps the first K-tile's.
+  f32x2* ln_rows = (f32x2*)(smem + SMEM2_BYTES);
+  f32x2 lnp[STG == 3 ? LN_PMAX : 1];
+  if constexpr (STG == 3) {
+    const long row = m0 + tid;
+    const bool ok = tid < BMT && row < M;
+#pragma unroll
+    for (int p = 0; p < LN_PMAX; ++p)
+      lnp[p] = (ok && p < e.ln_parts) ? *(const f32x2*)(e.ln_stats + (row * e.ln_parts + p) * 2) : f32x2{0.f, 0.f};
+  }
   // prologue: K-tile 0 (all four halves) and B0 of K-tile 1
   issue(0, 0, 0);
   issue(0, 1, 0);
   issue(1, 0, 0);
   issue(1, 1, 0);
-  wait_dma(issue(1, 0, 1));
+  const bool b01 = issue(1, 0, 1);
+  if constexpr (STG == 3) {
+    if (tid < BMT) {  // Chan, partial p (64 columns) onto the first 64 p: weights 1 / (p + 1) are constants
+      float mu = 0.f, q = 0.f;
+#pragma unroll
+      for (int p = 0; p < LN_PMAX; ++p)
+        if (p < e.ln_parts) {
+          const float d = lnp[p][0] - mu, f = 1.0f / (float)(p + 1);
+          mu = fmaf(d, f, mu);
+          q += lnp[p][1] + d * d * (64.0f * (float)p * f);
+        }
+      const float rs = __builtin_amdgcn_rsqf(q / (64.0f * (float)e.ln_parts) + e.ln_eps);
+      ln_rows[tid] = f32x2{rs, -rs * mu};
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible to every wave past the next barrier
+    }
+  }
+  wait_dma(b01);
   bar_raw();
   if (wr == 1) bar_raw();  // stagger: group 1 runs one barrier behind group 0
 
@@ -1200,7 +1185,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
         const int buf = wr == 0 ? (nk & 1) : ((nk - 1) & 1);
         char* stg = smem + buf * BUF_BYTES + wc * 16384;
         stage_epilogue<ACT, DROP, STG == 2 || STG == 4, STG == 3 ? 1 : (STG == 4 ? 2 : 0)>(
-            acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane, stg);
+            acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane, stg, ln_rows + wr * HR);
         return;
       }
     }
@@ -1608,7 +1593,7 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
     }
     if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
       if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 4>, SMEM2_BYTES);
-      if constexpr (!DROP) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 3>, SMEM2_BYTES);
+      if constexpr (!DROP) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 3>, SMEM2_LN_BYTES);
     }
     attr = true;
   }
@@ -1616,7 +1601,7 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
   if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {  // LayerNorm fold / statistics (mit_gemm checked them)
     if constexpr (!DROP) {
       if (e.ln_stats) {
-        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 3>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 3>), grid, dim3(512), SMEM2_LN_BYTES, s, (const bf16*)g->A,
                            (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
                            (float*)g->workspace, g->rowsum);
         return;
