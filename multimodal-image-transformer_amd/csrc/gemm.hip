@@ -695,7 +695,8 @@ constexpr int BUF_BYTES = 4 * HALF_BYTES;
 constexpr int EPI_LD = 68;                // per-wave fp32 epilogue stage [64][68]
 constexpr int SMEM2_BYTES = (2 * BUF_BYTES > 8 * 64 * EPI_LD * 4) ? 2 * BUF_BYTES : 8 * 64 * EPI_LD * 4;
 constexpr int LN_PMAX = 16;                                 // LN fold: statistics partials per row (K <= 1024)
-constexpr int SMEM2_LN_BYTES = SMEM2_BYTES + 256 * 8;       // + the tile's per-row (rstd, -rstd mean)
+constexpr int SMEM2_EPI_BYTES = SMEM2_BYTES + 4096;  // staged epilogues: + the tile's per-row (rstd, -rstd mean),
+                                                     // per-column bias and LN-fold column sums
 
 // Per-lane LDS-DMA source plan for one operand (8 waves x 2 wave-instructions per half-tile):
 // byte offsets of this lane's two 16-B chunks in each half at K-tile 0 (OOB when the row / column
@@ -830,29 +831,25 @@ __device__ __forceinline__ float sum_rows(float v) {
 // (rstd, -rstd mean) from lnrow: merged once per tile row in the kernel's prologue, ln_rows); 2 = also
 // write the per-64-column (mean, M2) of the bf16-rounded output rows to e.stats_out (the next LayerNorm's
 // statistics: this wave's 64 columns are one partial)
+// lcol: the wave's 64 columns' bias (lcol[0, 64)) and, LNX 1, folded-weight column sums (lcol[256, 320)),
+// staged in LDS by the kernel's prologue (zero past N)
 template <int ACT, bool DROP, bool XOPS, int LNX = 0>
 __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const Epi& e, void* C, long ldc, long M,
-                                               long N, long mw, long nw, int lane, char* stg,
+                                               long N, long mw, long nw, int lane, char* stg, const float* lcol,
                                                const f32x2* lnrow = nullptr) {
   constexpr int PASSES = 1, IP = 8;  // one pass over the wave's 8 16-row blocks
   const int g = lane >> 4, r16 = lane & 15;
   float bj[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const long c = nw + 16 * j + 4 * g;
-    if (e.bias && c < N) {
-      const f32x4 b = *(const f32x4*)(e.bias + c);
-      bj[j][0] = b[0]; bj[j][1] = b[1]; bj[j][2] = b[2]; bj[j][3] = b[3];
-    } else {
-      bj[j][0] = bj[j][1] = bj[j][2] = bj[j][3] = 0.f;
-    }
+    const f32x4 b = *(const f32x4*)(lcol + 16 * j + 4 * g);
+    bj[j][0] = b[0]; bj[j][1] = b[1]; bj[j][2] = b[2]; bj[j][3] = b[3];
   }
   float sj[LNX == 1 ? 4 : 1][4];  // LN fold: the column sums of the folded weight rows
   if constexpr (LNX == 1) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const long c = nw + 16 * j + 4 * g;
-      const f32x4 b = c < N ? *(const f32x4*)(e.ln_colsum + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 b = *(const f32x4*)(lcol + 256 + 16 * j + 4 * g);
       sj[j][0] = b[0]; sj[j][1] = b[1]; sj[j][2] = b[2]; sj[j][3] = b[3];
     }
   }
@@ -1089,6 +1086,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
   // K loop's counted vmcnt waits (younger DMAs only) stay exact, and the merge after the prologue's DMA
   // issue waits for them alone; their round trip overlaps the first K-tile's.
   f32x2* ln_rows = (f32x2*)(smem + SMEM2_BYTES);
+  // staged epilogues: the tile's 256 bias values (and LN-fold column sums) loaded here too, into LDS
+  float* lcol = (float*)(smem + SMEM2_BYTES + 2048);
+  float pbias = 0.f, pcols = 0.f;
+  if constexpr (STG != 0) {
+    const long c = n0 + tid;
+    if (tid < B2 && c < N) {
+      if (e.bias) pbias = e.bias[c];
+      if constexpr (STG == 3) pcols = e.ln_colsum[c];
+    }
+  }
   f32x2 lnp[STG == 3 ? LN_PMAX : 1];
   if constexpr (STG == 3) {
     const long row = m0 + tid;
@@ -1115,8 +1122,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
         }
       const float rs = __builtin_amdgcn_rsqf(q / (64.0f * (float)e.ln_parts) + e.ln_eps);
       ln_rows[tid] = f32x2{rs, -rs * mu};
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible to every wave past the next barrier
     }
+  }
+  if constexpr (STG != 0) {
+    if (tid < B2) {
+      lcol[tid] = pbias;
+      if constexpr (STG == 3) lcol[256 + tid] = pcols;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // visible to every wave past the next barrier
   }
   wait_dma(b01);
   bar_raw();
@@ -1185,7 +1198,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
         const int buf = wr == 0 ? (nk & 1) : ((nk - 1) & 1);
         char* stg = smem + buf * BUF_BYTES + wc * 16384;
         stage_epilogue<ACT, DROP, STG == 2 || STG == 4, STG == 3 ? 1 : (STG == 4 ? 2 : 0)>(
-            acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane, stg, ln_rows + wr * HR);
+            acc, e, C, ldc, M, N, m0 + wr * HR, n0 + wc * 64, lane, stg, lcol + wc * 64, ln_rows + wr * HR);
         return;
       }
     }
@@ -1588,12 +1601,12 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
   if (!attr) {
     set_lds(gemm256_kernel<AL, BL, ACT, DROP>, SMEM2_BYTES);
     if constexpr (AL == MIT_K_CONTIG) {
-      set_lds(gemm256_kernel<AL, BL, ACT, DROP, 1>, SMEM2_BYTES);
-      if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 2>, SMEM2_BYTES);
+      set_lds(gemm256_kernel<AL, BL, ACT, DROP, 1>, SMEM2_EPI_BYTES);
+      if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 2>, SMEM2_EPI_BYTES);
     }
     if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {
-      if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 4>, SMEM2_BYTES);
-      if constexpr (!DROP) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 3>, SMEM2_LN_BYTES);
+      if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 4>, SMEM2_EPI_BYTES);
+      if constexpr (!DROP) set_lds(gemm256_kernel<AL, BL, ACT, DROP, 3>, SMEM2_EPI_BYTES);
     }
     attr = true;
   }
@@ -1601,7 +1614,7 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
   if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {  // LayerNorm fold / statistics (mit_gemm checked them)
     if constexpr (!DROP) {
       if (e.ln_stats) {
-        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 3>), grid, dim3(512), SMEM2_LN_BYTES, s, (const bf16*)g->A,
+        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 3>), grid, dim3(512), SMEM2_EPI_BYTES, s, (const bf16*)g->A,
                            (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
                            (float*)g->workspace, g->rowsum);
         return;
@@ -1609,7 +1622,7 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
     }
     if constexpr (ACT == MIT_ACT_NONE) {
       if (e.stats_out) {
-        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 4>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 4>), grid, dim3(512), SMEM2_EPI_BYTES, s, (const bf16*)g->A,
                            (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
                            (float*)g->workspace, g->rowsum);
         return;
@@ -1621,14 +1634,14 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
     if (epi_gatherable(e) && !e.out_f32) {
       if constexpr (ACT == MIT_ACT_NONE) {
         if (ops) {
-          hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 2>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+          hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 2>), grid, dim3(512), SMEM2_EPI_BYTES, s, (const bf16*)g->A,
                              (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
                              (float*)g->workspace, g->rowsum);
           return;
         }
       }
       if (!ops) {
-        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 1>), grid, dim3(512), SMEM2_BYTES, s, (const bf16*)g->A,
+        hipLaunchKernelGGL((gemm256_kernel<AL, BL, ACT, DROP, 1>), grid, dim3(512), SMEM2_EPI_BYTES, s, (const bf16*)g->A,
                            (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e,
                            (float*)g->workspace, g->rowsum);
         return;
