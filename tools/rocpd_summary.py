@@ -44,7 +44,9 @@ def sq_pass(db):
     quantities derived from them (MI355X_MICROARCH.md):
       eff_clock_ghz   = GRBM_GUI_ACTIVE / 8 XCDs / dispatch wall time (reads high below ~0.3 ms dispatches)
       mfma_busy_frac  = SQ_VALU_MFMA_BUSY_CYCLES (summed over the 1024 SIMDs) / (1024 x GRBM_GUI_ACTIVE / 8),
-                        the share of SIMD-cycles of the dispatch in which the MFMA pipe was busy"""
+                        the share of SIMD-cycles of the dispatch in which the MFMA pipe was busy
+      mfma_busy_of_peak = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x wall x 2.4 GHz): the same busy cycles against
+                        the nominal clock (no GRBM window: the fraction of the dense MFMA peak kept busy)"""
     c = sqlite3.connect(db)
     rows = c.execute("select kernel_name, counter_name, count(*), avg(value), avg(duration) from counters_collection "
                      "group by kernel_name, counter_name").fetchall()
@@ -59,6 +61,7 @@ def sq_pass(db):
             e["eff_clock_ghz"] = round(cyc / e["avg_ns"], 3)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in e:
                 e["mfma_busy_frac"] = round(e["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc), 4)
+                e["mfma_busy_of_peak"] = round(e["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * e["avg_ns"] * 2.4), 4)
             if "SQ_BUSY_CYCLES" in e:
                 e["sq_busy_frac"] = round(e["SQ_BUSY_CYCLES"] / (8.0 * cyc), 4)
     return out
