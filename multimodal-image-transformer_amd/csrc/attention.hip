@@ -566,6 +566,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
     const char* Kc = Ks;
     const char* Vc = Vs;
     int j0 = 0;
+    const int ilk = (int)Lk;
     for (; j0 + 64 <= lkp; j0 += 64, Kc += 64 * 128, Vc += 64 * 128) {
       // ---- S^T = K Q^T for keys j0 .. j0+63 (4 key tiles of 16) ----
       f32x4 st[4];
@@ -593,10 +594,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
       for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
         for (int t = 0; t < 4; ++t) s[nb * 4 + t] = st[nb][t];
-      if (j0 + 64 > Lk) {  // ragged last chunk (wave-uniform)
+      // ragged last chunk (wave-uniform; 32-bit compares, and a real branch: left to the compiler it was
+      // if-converted into 48 64-bit compare / select VALU ops in every chunk, ~35 % of the chunk's VALU --
+      // measured neutral on this latency-bound loop, CLIP-L/14@336 48.3 -> 47.6 us)
+      if (__builtin_expect(j0 + 64 > ilk, 0)) {
+        const int live = ilk - j0 - g * 4;
 #pragma unroll
         for (int k = 0; k < 16; ++k)
-          if (j0 + (k >> 2) * 16 + g * 4 + (k & 3) >= Lk) s[k] = -INFINITY;
+          if ((k >> 2) * 16 + (k & 3) >= live) s[k] = -INFINITY;
       }
       // row max: v_max3 tree over the 16 in-lane scores, then the query's 4 lane groups (l, l ^ 16,
       // l ^ 32, l ^ 48) through v_permlane16/32_swap (VALU) instead of ds_bpermute round trips
