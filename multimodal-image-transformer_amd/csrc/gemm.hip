@@ -348,9 +348,6 @@ __device__ __forceinline__ void wait_tiles(int younger) {
   }
 }
 
-#ifndef MIT_G128_PP  // ping-pong K loop of the 8-wave 128 kernel (compile-time A/B)
-#define MIT_G128_PP 0
-#endif
 // NST = LDS stages (K-tiles resident at once). Launched with 2 (64 KiB: two blocks per CU). Four
 // stages (three tiles in flight) on the 1-block-per-CU decoder grids measured no faster (within
 // 2 %, tools/gemm_bench.py): those blocks are bound by per-iteration latency, not DMA depth.
@@ -424,72 +421,6 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
     }
   };
 
-#if MIT_G128_PP
-  // Ping-pong K loop (8 waves, 2 LDS stages): each K-tile is a read phase R (all of the wave's fragments of
-  // the tile -> registers) and an MFMA phase M, separated by barriers, with waves 4-7 (G1) one barrier behind
-  // waves 0-3 (G0) -- wave w and w + 4 share a SIMD, so one runs its MFMAs while its partner reads LDS.
-  // Barrier pairing: G0 X(k) <-> G1 Y(k-1), G0 Y(k) <-> G1 X(k). Tile t's DMA (into buffer t & 1) goes out
-  // once both groups' reads of tile t-2 returned: G0 in R(t-1), G1 in M(t-2); each wave waits for its own
-  // pieces of a tile before the barrier that releases that tile's first reader.
-  if constexpr (NST == 2 && NW == 8) {
-    const bool g1 = wid >= 4;
-    auto dma = [&](int t) {
-      glds_tile<ALAY, 16 / NW>(ra, AS(t & 1), lda, M, ke, m0, kb + (long)t * BK, wid, lane);
-      glds_tile<BLAY, 16 / NW>(rb, BS(t & 1), ldb, N, ke, n0, kb + (long)t * BK, wid, lane);
-    };
-    bf16x8 af[2][MI], bfr[2][4];
-    auto reads = [&](int cur) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i) af[kk][i] = frag<ALAY>(AS(cur), wm * WR + i * 16, kk, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[kk][j] = frag<BLAY>(BS(cur), wn * 64 + j * 16, kk, lane);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    };
-    auto mfmas = [&]() {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
-        if (do_rs) {
-#pragma unroll
-          for (int i = 0; i < MI; ++i) rs[i] = frag_rowsum(af[kk][i], rs[i]);
-        }
-      }
-    };
-    if (nk > 0) dma(0);
-    if (g1) {
-      if (nk > 1) dma(1);
-      wait_tiles<NST, 2 * (16 / NW)>(nk > 1 ? 1 : 0);  // own pieces of tile 0 (tile 1 may be in flight)
-      bar_raw();                                       // E: pairs with G0's X(0)
-      for (int kt = 0; kt < nk; ++kt) {
-        bar_raw();  // X(kt) <-> G0 Y(kt)
-        reads(kt & 1);
-        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own pieces of tile kt+1
-        bar_raw();  // Y(kt) <-> G0 X(kt+1)
-        if (kt + 2 < nk) dma(kt + 2);  // both groups' reads of tile kt returned
-        mfmas();
-      }
-    } else {
-      for (int kt = 0; kt < nk; ++kt) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own pieces of tile kt
-        bar_raw();  // X(kt) <-> G1 Y(kt-1) (kt = 0: G1's E)
-        if (kt >= 1 && kt + 1 < nk) dma(kt + 1);  // both groups' reads of tile kt-1 returned
-        if (kt == 0 && nk > 1) dma(1);
-        reads(kt & 1);
-        bar_raw();  // Y(kt) <-> G1 X(kt)
-        mfmas();
-      }
-      bar_raw();  // re-align: pairs with G1's Y(nk-1)
-    }
-    __syncthreads();
-  } else
-#endif
   {
   // LDS-DMA, NST stages: NST-1 tiles' DMA in flight while one computes; counted vmcnt (8 DMAs per
   // tile per wave) + raw barriers (a __syncthreads() would drain the in-flight DMA with vmcnt(0), guide §5)
