@@ -39,9 +39,13 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
+// one lowbias32 round over the element index keyed by (seed, site): the key's two halves fold into one
+// wave-uniform word (scalar work), the index's high half (0 below 2^32 elements) is added before the
+// round. Was two rounds (the second mixing the high halves): the decoder's dropout sites hash every
+// element they touch, forward and backward, so the round is VALU on the critical kernels.
 __device__ __forceinline__ uint32_t mix_u32(uint64_t key, uint64_t idx) {
-  uint32_t x = lowbias32((uint32_t)idx ^ (uint32_t)key);
-  return lowbias32(x ^ (uint32_t)(idx >> 32) ^ (uint32_t)(key >> 32));
+  const uint32_t k = (uint32_t)key ^ ((uint32_t)(key >> 32) * 0x9E3779B9u);
+  return lowbias32(((uint32_t)idx ^ k) + (uint32_t)(idx >> 32) * 0x85EBCA6Bu);
 }
 __device__ __forceinline__ uint64_t site_key(const uint64_t* seed, uint32_t site) {
   return (seed ? *seed : 0ull) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(site + 1));
