@@ -245,6 +245,16 @@ class ImageToTextModel:
         ev = self._enc_events.record(enc)
         self._prefetched = (images, slot, out, ev)
 
+    def _take_encoded(self, images: torch.Tensor):
+        """The encoder rows for images: the prefetched ones when they are for these images (this stream
+        waits for them), else computed here into the current arena."""
+        pf, self._prefetched = self._prefetched, None
+        if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
+            _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
+            native.HipEvents.wait(native.stream_ptr(), ev)
+            return enc_rows, enc_ld, S
+        return self._encoder_rows(images, self._enc_slot)
+
     def _encode_memory(self, images: torch.Tensor, refresh: bool = True):
         """Returns (mem_rows, mem_ld, S, enc_rows, enc_ld): memory [B*S rows of d] and the
         encoder features that feed the projection (for its weight gradient). refresh: re-cast the
@@ -253,12 +263,7 @@ class ImageToTextModel:
         E, d = self.encoder.E, self.decoder_embed_dim
         self.store.ensure_shadow(force=refresh)
         self._gen += 1
-        pf, self._prefetched = self._prefetched, None
-        if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
-            _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
-            native.HipEvents.wait(native.stream_ptr(), ev)
-        else:
-            enc_rows, enc_ld, S = self._encoder_rows(images, self._enc_slot)
+        enc_rows, enc_ld, S = self._take_encoded(images)
         self._slot_freed[self._enc_slot] = False  # re-armed by _train_step once this step's readers are issued
         if not self.has_projection:
             return enc_rows, enc_ld, S, enc_rows, enc_ld
@@ -303,12 +308,7 @@ class ImageToTextModel:
         B, T = tokens.shape
         self.store.ensure_shadow(force=True)
         self._gen += 1
-        pf, self._prefetched = self._prefetched, None
-        if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
-            _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
-            native.HipEvents.wait(native.stream_ptr(), ev)
-        else:
-            enc_rows, enc_ld, S = self._encoder_rows(images, self._enc_slot)
+        enc_rows, enc_ld, S = self._take_encoded(images)
         E = self.encoder_output_dim
         # the encoder arena is reused by the next forward: the projection's saved input is a copy
         enc = torch.as_strided(enc_rows, (B * S, E), (enc_ld, 1)).clone()
