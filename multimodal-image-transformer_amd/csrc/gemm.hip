@@ -367,19 +367,29 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
 
   const int nbn = (int)((N + BN - 1) / BN), nbm = (int)((M + BM - 1) / BM);
   const int ntiles = nbn * nbm, nwg = ntiles * ksplit;
-  int bid = xcd_remap(blk, nwg);
+  // GROUP = 0 (the grouped dW launch): blk is already the tile's index in its problem's XCD-piece
+  // order (grouped_tile), no remap
+  int bid = GROUP ? xcd_remap(blk, nwg) : blk;
   // split-K: slice `split` covers k in [kb, ke); a tile's slices are neighbours in the remapped
   // order, i.e. on one XCD
   const int split = bid % ksplit;
   bid /= ksplit;
   const long kb = (long)split * kchunk, ke = min(K, kb + kchunk);
-  // groups of GROUP M-blocks walk the N-blocks together (B panel reuse in L2); GROUP = 1: row-major
-  // tiles, so an XCD's contiguous run of tiles shares its A row panels (the grouped dW launch)
-  const int group_id = bid / (GROUP * nbn);
-  const int first_m = group_id * GROUP;
-  const int gsize = min(nbm - first_m, GROUP);
-  const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
-  const int bn = (bid % (GROUP * nbn)) / gsize;
+  int bm, bn;
+  if (GROUP) {
+    // groups of GROUP M-blocks walk the N-blocks together (B panel reuse in L2)
+    const int group_id = bid / (GROUP * nbn);
+    const int first_m = group_id * GROUP;
+    const int gsize = min(nbm - first_m, GROUP);
+    bm = first_m + (bid % (GROUP * nbn)) % gsize;
+    bn = (bid % (GROUP * nbn)) / gsize;
+  } else if (nbn <= nbm) {  // the shorter side fastest: a contiguous run of tiles is a compact block
+    bm = bid / nbn;
+    bn = bid % nbn;
+  } else {
+    bm = bid % nbm;
+    bn = bid / nbm;
+  }
   const long m0 = (long)bm * BM, n0 = (long)bn * BN;
   MIT_DASSERT(blk < nwg && split < ksplit && bm < nbm && bn < nbn && m0 < M && n0 < N);
   MIT_DASSERT(lda >= (ALAY == MIT_K_CONTIG ? K : M) && ldb >= (BLAY == MIT_K_CONTIG ? K : N) && ldc >= N);
@@ -549,10 +559,20 @@ struct GroupLn {
   long nblk, cols;
   int start;
 };
+// XCD pieces of a grouped launch: block b runs on XCD b % 8 (round-robin dispatch), as its (b / 8)-th
+// block there. The host deals each problem's tiles (in the order of gemm_bf16_body's GROUP = 0 branch)
+// to the XCDs in contiguous runs of at most ceil(tiles / 8), so one XCD's L2 holds few problems and
+// compact tile blocks of them (their dY / X panels read once per XCD, not once per XCD per problem).
+constexpr int MAXP = MAXG + 8;
+struct GroupPiece {
+  int prob, t0, count;
+};
 struct GroupArgs {
   GroupProb p[MAXG];
   GroupLn ln[MAXLN];
-  int n, nln, gemm_blocks, group;
+  GroupPiece pc[MAXP];
+  int xfirst[9];  // pieces of XCD x: [xfirst[x], xfirst[x + 1])
+  int n, nln, gemm_blocks;
 };
 
 __device__ __forceinline__ void ln_grads_block(const GroupLn& j, int blk) {
@@ -585,14 +605,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_grouped(GroupArgs ga) {
     ln_grads_block(ga.ln[j], (int)blockIdx.x - ga.ln[j].start);
     return;
   }
-  int i = 0;
-  while (i + 1 < ga.n && (int)blockIdx.x >= ga.p[i + 1].start) ++i;
-  const GroupProb& q = ga.p[i];
-  // weight gradients dW = dY^T X with K = B*T: the dY column panel (K x 128, the A operand) of a
-  // tile row is read once when that row's tiles sit on one XCD (GROUP 1)
+  const int x = (int)blockIdx.x & 7;
+  int slot = (int)blockIdx.x >> 3, j = ga.xfirst[x];
+  while (j < ga.xfirst[x + 1] && slot >= ga.pc[j].count) slot -= ga.pc[j++].count;
+  if (j == ga.xfirst[x + 1]) return;  // this XCD's share is shorter than the longest
+  const GroupProb& q = ga.p[ga.pc[j].prob];
+  // weight gradients dW = dY^T X with K = B*T
   gemm_bf16_body<MIT_MN_CONTIG, MIT_MN_CONTIG, MIT_ACT_NONE, false, 2, 8>(
       q.A, q.B, q.C, q.M, q.N, q.K, q.lda, q.ldb, q.ldc, q.a_bytes, q.b_bytes, q.e, q.ksplit, q.kchunk, q.ws, q.rowsum,
-      (int)blockIdx.x - q.start, ga.group);
+      ga.pc[j].t0 + slot, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1877,7 +1898,6 @@ extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, const mit_ln_g
   const long s = grouped_split(tiles);
   GroupArgs ga;
   ga.n = n;
-  ga.group = 1;  // row-major tiles: an XCD's run of tiles shares the dY panel (FETCH 248 -> 225 MB)
   int start = 0, rstart = 0;
   bool any_split = false;
   char* wsp = (char*)workspace + WS_HDR;
@@ -1922,6 +1942,26 @@ extern "C" int mit_gemm_grouped(const mit_gemm_args* args, int n, const mit_ln_g
     set_lds(gemm_bf16_grouped, smem_bytes(2));
     attr = true;
   }
+  // deal the tiles to the XCDs: problem after problem, at most cap per XCD
+  const int cap = (start + 7) / 8;
+  int np = 0, xc = 0, used = 0;
+  ga.xfirst[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const int ti = (i + 1 < n ? ga.p[i + 1].start : start) - ga.p[i].start;
+    for (int t = 0; t < ti;) {
+      const int take = min(ti - t, cap - used);
+      ga.pc[np++] = GroupPiece{i, t, take};
+      t += take;
+      used += take;
+      if (used == cap) {
+        ga.xfirst[++xc] = np;
+        used = 0;
+      }
+    }
+  }
+  while (xc < 8) ga.xfirst[++xc] = np;
+  MIT_CHECK_ARG(np <= MAXP, "mit_gemm_grouped: %d XCD pieces", np);
+  start = 8 * cap;
   ga.gemm_blocks = start;
   ga.nln = n_ln;
   for (int j = 0; j < n_ln; ++j) {

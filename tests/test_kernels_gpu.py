@@ -426,14 +426,17 @@ def test_cross_entropy_row_kernel(V, want_grad):
         assert torch.equal(g, logits)
 
 
-@pytest.mark.parametrize("R", [4032, 520])
-def test_gemm_grouped_weight_gradients_match_single_launches(R):
+@pytest.mark.parametrize("R,kind", [(4032, "layer"), (520, "layer"), (3000, "tail"), (2048, "one")])
+def test_gemm_grouped_weight_gradients_match_single_launches(R, kind):
     """mit_gemm_grouped (a decoder layer's six dW = dY^T X + bias row sums in one launch, split-K chosen
-    for the group) against float64 torch, and against the one-GEMM-per-problem launches."""
+    for the group; the tiles dealt to the XCDs in per-problem runs) against float64 torch, and against
+    the one-GEMM-per-problem launches. "tail": the cross-K/V + projection pair (split-K 2 on both);
+    "one": a single problem with split-K 10."""
     dev = torch.device("cuda")
     d, F = 512, 2048
     g = torch.Generator().manual_seed(R)
-    shapes = [(d, F), (F, d), (d, d), (d, d), (d, d), (3 * d, d)]  # (M = out features, N = in features)
+    shapes = {"layer": [(d, F), (F, d), (d, d), (d, d), (d, d), (3 * d, d)],  # (M = out features, N = in)
+              "tail": [(6 * d, d), (d, 768)], "one": [(d, 768)]}[kind]
     probs, refs = [], []
     for M, Nn in shapes:
         A = torch.randn(R, M, generator=g).to(dev, torch.bfloat16)
