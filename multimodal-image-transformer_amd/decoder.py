@@ -160,8 +160,9 @@ class _Acts:
         self.lse_c = [f(B * H * T) for _ in range(nl)]
         # per-layer normalised outputs x1, x2, x3 (x3 of layer l = input of layer l+1)
         self.xs = [[e(R, d) for _ in range(3)] for _ in range(L if train else 2)]
-        self.count = f(1)
-        self.loss_sum = f(1)
+        self.count_loss = f(2)  # {non-PAD target count, CE loss sum}: one memset per step
+        self.count = self.count_loss[0:1]
+        self.loss_sum = self.count_loss[1:2]
         self.loss = f(1)
         self.row_loss = f(R)  # per-row CE losses (deterministic loss sum)
         # split-K scratch of the main stream: the d_model GEMMs (R x d outputs, 128 tiles at B = 64)
@@ -485,7 +486,10 @@ class TransformerDecoder:
         if side is None:
             native.embed_plan(tokens, A.emb_plan)
         else:
-            side.run(lambda: native.embed_plan(tokens, A.emb_plan))
+            # the embedding plan depends on the tokens only; the table gradient's zero fill (20 MB at
+            # cfg1) rides with it, off the main stream's chain (the previous AdamW, its last reader, is
+            # behind the side stream's wait on main)
+            side.run(lambda: (native.embed_plan(tokens, A.emb_plan), native.zero(g("token_embedding.weight"))))
             plan_ev = side.plan_events.record(side.ptr)
 
         def dW(dy, x, wname, bname, M, N, K, lda, ldb):
@@ -620,9 +624,10 @@ class TransformerDecoder:
             dW(A.dkv, mem, "cross_kv.weight", "cross_kv.bias", L * 2 * d, d, BS, L * 2 * d, mem_ld)
         # embedding (scatter-add into a zeroed table gradient; PAD row gets nothing)
         ge = g("token_embedding.weight")
-        native.zero(ge)
         if side is not None:
-            native.HipEvents.wait(native.stream_ptr(), plan_ev)
+            native.HipEvents.wait(native.stream_ptr(), plan_ev)  # the plan and the zeroed table
+        else:
+            native.zero(ge)
         native.embed_bwd(tokens, A.dx, math.sqrt(d), ge, self.pad_idx, drop_p=p, seed=seed, site=EMB_SITE,
                          plan=A.emb_plan)
         last = "token_embedding.weight"

@@ -359,8 +359,7 @@ class ImageToTextModel:
         A = dec.acts(B, T, S, True)
         native.step_inc(self.seed_t)
         logits, _ = dec.run_forward(tokens, mem, mem_ld, S, A, self.seed_t, True, tick=tick)
-        native.zero(A.count)
-        native.zero(A.loss_sum)
+        native.zero(A.count_loss)
         native.count_targets(targets, self.decoder_pad_idx, A.count)
         if dist is not None:
             dist.all_reduce_count(A.count)
