@@ -327,13 +327,15 @@ def decode_throughput(args, launch=None):
     if launch:
         os.environ["MIT_DECODE_LAUNCH"] = launch
     try:
+        # the next call's encoder runs beside this call's token steps (generate_batch next_images)
+        nxt = None if getattr(args, "no_prefetch", False) else images
         for _ in range(max(1, args.warmup // 2)):
-            model.generate_batch(images, 2, never, max_len=args.max_len)
+            model.generate_batch(images, 2, never, max_len=args.max_len, next_images=nxt)
         torch.cuda.synchronize()
         K = max(1, args.steps // 4)
         t0 = time.perf_counter()
         for _ in range(K):
-            ids = model.generate_batch(images, 2, never, max_len=args.max_len)
+            ids = model.generate_batch(images, 2, never, max_len=args.max_len, next_images=nxt)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
     finally:
@@ -362,7 +364,8 @@ def bench_decode(args):
            "value": d["value"], "unit": "tokens/s", "n_gpus": 1, "steps": d["calls"], "warmup": max(1, args.warmup // 2),
            "ms_per_step": d["ms_per_call"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
            "dtype": args.dtype, "data": "synthetic (randn 224x224 images; random-init weights)",
-           "config": {"workload": "configs[4]: inference.py greedy decode, cached cross-attn K/V, " + DECODE_LAUNCH_NOTE,
+           "config": {"workload": "configs[4]: inference.py greedy decode, cached cross-attn K/V, the next call's "
+                                      "encoder issued beside the token steps (--no-prefetch: inline), " + DECODE_LAUNCH_NOTE,
                       "images": d["images"], "max_len": args.max_len, "memory_mode": "patches"},
            "images_per_s": d["images_per_s"], "us_per_token_step": d["us_per_token_step"],
            "ids_per_caption": d["ids_per_caption"]}
@@ -475,7 +478,8 @@ def main():
                     help="issue every step from Python (eager launches). Default: the step's launches are recorded "
                          "once (native.record, mit_plan_*) and replayed from C++ per step, same streams and order")
     ap.add_argument("--no-prefetch", action="store_true",
-                    help="run the frozen encoder inside each step instead of one step ahead on a second stream")
+                    help="run the frozen encoder inside each step (train) / call (decode) instead of one ahead on a "
+                         "second stream")
     ap.add_argument("--workload", default="train", choices=["train", "clip336", "cfg3", "decode"],
                     help="train: the BASELINE metric (default, configs[1]). clip336 / cfg3: the one-GPU share of "
                          "configs[2] / configs[3] (same step, CLIP-L encoders). decode: configs[4], batched greedy "

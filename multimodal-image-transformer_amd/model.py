@@ -457,7 +457,8 @@ class ImageToTextModel:
 
     @torch.no_grad()
     def generate_batch(self, images, start_token_id: int, end_token_id: int, max_len: int = 100,
-                       use_graph: bool = True, check_every: int = 8, streams: Optional[int] = None) -> List[List[int]]:
+                       use_graph: bool = True, check_every: int = 8, streams: Optional[int] = None,
+                       next_images: Optional[torch.Tensor] = None) -> List[List[int]]:
         """Greedy captions for a whole batch (BASELINE config 5): per image the same token list as
         generate() (model.py:171-242: START, argmax of the last position each step, stop after END,
         at most max_len ids), computed with cached self-attention K/V, the cross-attention K/V of
@@ -469,7 +470,11 @@ class ImageToTextModel:
         greedy decoding and every kernel computes a row the same way at any batch size, so the ids
         do not depend on the grouping. Measured at B = 256 (configs[4]): 2 / 3 / 4 groups take 1.12 /
         1.23 / 1.53x the one-group time -- the groups' kernels do overlap, but every kernel boundary
-        costs the same whatever its size, so one group of full-width launches is fastest."""
+        costs the same whatever its size, so one group of full-width launches is fastest.
+
+        next_images: the next call's images (pixel values on the device); their frozen encoder forward is
+        issued on the encoder stream one launch chunk per token step, beside this call's latency-bound
+        token steps, and the next call takes it (as train_step's next_images; the ids are unchanged)."""
         self.eval()
         pv = images if isinstance(images, torch.Tensor) else \
             self.image_processor(images=images, return_tensors="pt")["pixel_values"]
@@ -520,13 +525,19 @@ class ImageToTextModel:
                 run = prog.run
             else:
                 run = one_step
+            pf = self.prefetch_encoder_iter(next_images) if next_images is not None else None
             while done < steps:
                 n = min(check_every, steps - done)
                 for _ in range(n):
                     run()
+                    # one encoder chunk per token step (one per 3 or 6 steps measured the same)
+                    if pf is not None and next(pf, pf) is pf:
+                        pf = None
                 done += n
                 if sum(int(stt.n_finished.item()) for stt in states) == B:
                     break
+            for _ in pf or ():
+                pass
             for s_ in side[1:]:
                 cur.wait_stream(s_)
         out = []

@@ -464,3 +464,25 @@ def test_generate_batch_plan_graph_eager_agree_with_two_streams(dtype, monkeypat
         got[launch] = m.generate_batch(imgs, 2, never, max_len=20, streams=2)
     one = m.generate_batch(imgs, 2, never, max_len=20, streams=1)
     assert got["plan"] == got["graph"] == got["eager"] == one
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_generate_batch_encoder_prefetch_equals_inline(dtype):
+    """generate_batch(next_images=...) issues the next call's encoder beside this call's token steps
+    (one launch chunk per step, into the other arena); the next call takes it. Ids equal the calls
+    without prefetch, across different batches, a stale prefetch (next call on other images) and a
+    call that stops early (every caption finished before the chunks ran out)."""
+    m, meta, _ = _trained("tiny_vit_patches", dtype)
+    img = FX.inputs(meta, 0)[0].cuda()
+    batches = [torch.cat([img, img.flip(-1)], 0), torch.cat([img * 0.5, img.flip(-2)], 0), torch.cat([-img, img], 0)]
+    never = 10 ** 6
+    ref = [m.generate_batch(b, 2, never, max_len=20) for b in batches]
+    ref_short = m.generate_batch(batches[0], 2, never, max_len=5)
+    got = [m.generate_batch(batches[0], 2, never, max_len=20, next_images=batches[1]),
+           m.generate_batch(batches[1], 2, never, max_len=20, next_images=batches[0]),  # stale: next is batches[2]
+           m.generate_batch(batches[2], 2, never, max_len=20, next_images=batches[0])]
+    short = m.generate_batch(batches[0], 2, never, max_len=5, next_images=batches[1])  # 4 steps < the chunks
+    after = m.generate_batch(batches[1], 2, never, max_len=20)
+    assert got == ref
+    assert short == ref_short
+    assert after == ref[1]
