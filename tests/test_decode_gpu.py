@@ -158,17 +158,20 @@ def test_generate_batch_bf16_consistent_with_full_forward():
 
 def test_generate_captions_postprocessed_like_reference():
     """inference.generate_captions (batched) == the reference's inference.py post-processing of its
-    own greedy ids (fixture), for both images at once; and load_model restores a saved state."""
+    own greedy ids (fixture), for both images at once and one per batch."""
     import inference
     m, meta, T = _trained("tiny_vit_cls", torch.float32)
     g = meta["generate"]
     imgs = torch.cat([T["gen.pixel_values0"], T["gen.pixel_values1"]], 0)
-    got = inference.generate_captions(m, imgs, decode=lambda ids: " ".join(f"t{i}" for i in ids),
-                                      start_token_id=g["start"], end_token_id=g["end"], max_len=g["max_len"])
-    for (ids, text), ref in zip(got, g["ids"]):
-        want = inference.postprocess_ids(ref, g["start"], g["end"])
-        assert ids == want
-        assert text == " ".join(f"t{i}" for i in want)
+    for bs in (256, 1):  # one batch; one image per batch (the second's encoder prefetched beside the first)
+        got = inference.generate_captions(m, imgs, decode=lambda ids: " ".join(f"t{i}" for i in ids),
+                                          start_token_id=g["start"], end_token_id=g["end"], max_len=g["max_len"],
+                                          batch_size=bs)
+        assert len(got) == 2
+        for (ids, text), ref in zip(got, g["ids"]):
+            want = inference.postprocess_ids(ref, g["start"], g["end"])
+            assert ids == want, bs
+            assert text == " ".join(f"t{i}" for i in want)
 
 
 def _cfg1_gen_model(dtype):
