@@ -205,9 +205,11 @@ def test_generate_batch_b256_cfg1_matches_reference_ids():
 def test_generate_batch_b256_bf16_agrees_with_full_forward():
     """bf16 batched KV-cache decode (the configs[4] benchmark path) at B = 256, max_len 100: every
     generated token equals the argmax of the teacher-forced full forward (model.forward, the
-    reference's recompute path) on the generated prefix, up to each row's first bf16 near-tie (top-1 -
-    top-2 margin < 3e-2 of the full forward's logits; random-init weights give many: the reference's
-    own 4 images have margins down to 2.7e-3), after which the two paths see different prefixes."""
+    reference's recompute path) on the generated ids. The full forward sees the decode's own prefix
+    at every position, so ALL 256 x 99 positions are compared (none is skipped after a disagreement);
+    the only disagreements allowed are bf16 near-ties (top-1 - top-2 margin < 3e-2 of the full
+    forward's logits; random-init weights give some: the reference's own 4 images have margins down
+    to 2.7e-3), and they must stay rare."""
     meta, m = _cfg1_gen_model(torch.bfloat16)
     images = _gen_images(meta, 256).cuda()
     ids = torch.tensor(m.generate_batch(images, meta["start"], -1, max_len=100))
@@ -218,21 +220,12 @@ def test_generate_batch_b256_bf16_agrees_with_full_forward():
         margin = (top2.values[..., 0] - top2.values[..., 1]).cpu()
     del logits
     nxt = ids[:, 1:]
-    # after a disagreement the two paths see different prefixes: compare up to each row's first
-    # near-tie position
-    bad = 0
-    tied = 0
-    for b in range(256):
-        for t in range(99):
-            if am[b, t] != nxt[b, t]:
-                if margin[b, t] < 3e-2:
-                    tied += 1
-                    break
-                bad += 1
-                break
-    print(f"b256 bf16 decode: {tied} rows stopped at a near-tie, {bad} real disagreements")
+    differ = am != nxt
+    tied = int((differ & (margin < 3e-2)).sum())
+    bad = int((differ & (margin >= 3e-2)).sum())
+    print(f"b256 bf16 decode: {differ.numel()} positions, {tied} near-tie disagreements, {bad} real ones")
     assert bad == 0
-    assert tied <= 256 // 4
+    assert tied <= differ.numel() // 50  # measured: 271 of 25344 (1.1 %), 0 real
 
 
 # --- fused bf16 decode step (mit_decode_gemm, mit_greedy_pick_advance) ---------------------------
