@@ -376,7 +376,8 @@ typedef struct {
    * ord(value) << 32 | (0xFFFFFFFF - column) (ord: the order-preserving u32 image of an f32, NaN
    * largest), so the surviving key is the first maximal column (torch.argmax). bf16 A rows, no residual
    * or activation; C / z_out may be NULL. The keys must be 0 before the launch (mit_greedy_pick_keys
-   * leaves them 0). */
+   * leaves them 0). N need not be a multiple of 8 in this mode (any vocabulary: columns >= N never
+   * enter the maximum). */
   unsigned long long* argmax_keys;
 } mit_decode_gemm_args;
 int mit_decode_gemm(const mit_decode_gemm_args* args, void* stream);

@@ -80,6 +80,12 @@ ENCODER_WEIGHTS_PATH = os.environ.get("MIT_ENCODER_WEIGHTS", None)
 # bf16). "auto" = the 24-layer CLIP-L towers (configs[2] / configs[3]), where a bf16 stream doubles
 # the encoder's error; "on" / "off" force it.
 ENCODER_F32_RESIDUAL = os.environ.get("MIT_ENCODER_F32_RESIDUAL", "auto")
+# bf16 ViT towers on the bf16 stream: fold each pre-LN LayerNorm into the GEMM that consumes it
+# (encoder.fold_layernorm). "auto" = on where it applies; "off" keeps the explicit LayerNorm launches.
+ENCODER_FOLD_LN = os.environ.get("MIT_ENCODER_FOLD_LN", "auto")
+# A NaN / inf training loss (e.g. an all-PAD batch): "warn" (default; the reference trains on through it)
+# reports the first such batch of the epoch, "raise" stops train_one_epoch with NonFiniteLossError.
+NONFINITE_LOSS = os.environ.get("MIT_NONFINITE_LOSS", "warn")
 
 # Encoder geometry by model name (values of the HF configs the names resolve to).
 ENCODER_SPECS = {

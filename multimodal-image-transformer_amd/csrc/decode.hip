@@ -917,8 +917,10 @@ extern "C" int mit_decode_gemm(const mit_decode_gemm_args* g, void* stream) {
   MIT_CHECK_ARG(g->M >= 0 && g->N > 0 && g->K > 0, "mit_decode_gemm: bad extents M=%ld N=%ld K=%ld", g->M, g->N, g->K);
   MIT_CHECK_ARG(g->A && g->B, "mit_decode_gemm: null operand");
   MIT_CHECK_ARG(g->C || g->z_out || g->argmax_keys, "mit_decode_gemm: no output");
-  MIT_CHECK_ARG(g->K % 8 == 0 && g->N % 8 == 0 && g->ldb % 8 == 0 && g->lda >= g->K && g->ldb >= g->K,
-                "mit_decode_gemm: K, N, ldb must be multiples of 8 and lda/ldb >= K");
+  // N % 8: the 8-column output vectors; the argmax head writes no C (any vocabulary, columns >= N masked)
+  MIT_CHECK_ARG(g->K % 8 == 0 && (g->N % 8 == 0 || g->argmax_keys) && g->ldb % 8 == 0 && g->lda >= g->K &&
+                    g->ldb >= g->K,
+                "mit_decode_gemm: K, N (unless argmax_keys), ldb must be multiples of 8 and lda/ldb >= K");
   MIT_CHECK_ARG(g->act == MIT_ACT_NONE || g->act == MIT_ACT_RELU, "mit_decode_gemm: act %d unsupported", g->act);
   MIT_CHECK_ARG(g->r_mode >= 0 && g->r_mode <= 2, "mit_decode_gemm: bad r_mode %d", g->r_mode);
   const bool lna = g->a_stats != nullptr;

@@ -77,18 +77,37 @@ class VisionEncoder:
         self.kin = 3 * self.patch * self.patch
         self.kpad = _round8(self.kin)
         self.device, self.dtype = device, dtype
-        mode = str(getattr(config, "ENCODER_F32_RESIDUAL", "auto")).lower()
-        # f32 residual stream (bf16 compute only): z = h + sublayer(bf16) in f32, fused into the next
-        # LayerNorm (mit_layernorm_fwd_x32), as autocast keeps modeling_vit.py:312-323 / modeling_clip.py:379-393
-        self.res32 = dtype == torch.bfloat16 and (mode in ("on", "1", "true") or (mode == "auto" and self.L >= 24))
         # bf16 stream: each pre-LN sublayer's LayerNorm folded into the GEMM that consumes it (fold_layernorm):
         # no LayerNorm launch inside the tower, the statistics come from the producing GEMM's epilogue. ViT
         # towers only: on the 2-layer CLIP-336 cls fixture the folded path's largest logit error (0.039) left
         # the asserted 1.5x of the reference's own bf16 error (0.037) while its encoder rel-L2 improved
         # (5.40e-3 vs 5.54e-3); the deep CLIP-L towers run the f32 residual stream anyway
-        self.fold_ln = dtype == torch.bfloat16 and not self.res32 and self.E % 64 == 0 and self.kind == "vit"
+        self._fold_ok = (dtype == torch.bfloat16 and self.E % 64 == 0 and self.kind == "vit"
+                         and str(getattr(config, "ENCODER_FOLD_LN", "auto")).lower() not in ("off", "0", "false"))
         self.w: Dict[str, torch.Tensor] = {}
         self._ws = {}
+        self.configure_for(None)
+
+    def configure_for(self, memory_mode: Optional[str]):
+        """Pick the residual-stream precision for the decoder memory this encoder feeds (the model calls this
+        with its memory_mode). f32 residual stream (bf16 compute only): z = h + sublayer(bf16) in f32, fused
+        into the next LayerNorm (mit_layernorm_fwd_x32), as autocast keeps modeling_vit.py:312-323 /
+        modeling_clip.py:379-393. config.ENCODER_F32_RESIDUAL "auto" turns it on
+          - for the 24-layer CLIP-L towers (configs[2] / configs[3]): a bf16 stream doubles their error;
+          - in "cls" memory mode (model.py:141-151): the memory is ONE encoder row per image and the
+            S = 1 cross-attention passes its error to the logits undamped (patches mode averages it over
+            197 rows). tools/bf16_bisect.py on cfg0_b4_cls: logits rel-L2 9.64e-3 (1.20x the reference's
+            own bf16 error) with the bf16 stream, 8.53e-3 (1.06x) with the f32 one; encoder alone 7.26e-3
+            vs 6.26e-3 for the decoder alone. The bench path (patches) keeps the folded bf16 stream.
+        "on" / "off" force it."""
+        mode = str(getattr(config, "ENCODER_F32_RESIDUAL", "auto")).lower()
+        res32 = self.dtype == torch.bfloat16 and (
+            mode in ("on", "1", "true") or (mode == "auto" and (self.L >= 24 or memory_mode == "cls")))
+        if getattr(self, "res32", None) != res32:
+            self._ws = {}  # the arenas differ between the two streams
+        self.res32 = res32
+        self.fold_ln = self._fold_ok and not res32  # the folded operands exist whenever _fold_ok (load time)
+        return self
 
     # --- weights -----------------------------------------------------------------------------
     @property
@@ -166,7 +185,7 @@ class VisionEncoder:
         for k, v in w.items():
             is_mat = k.endswith(".w") and v.dim() == 2 and not k.endswith("ln.w")
             out[k] = v.to(device=dev, dtype=dt if is_mat else torch.float32).contiguous()
-        if self.fold_ln:
+        if self._fold_ok:  # from the f32 weights (one rounding of W o gamma), whichever stream runs now
             for i in range(self.L):
                 for mat, ln in (("qkv", "ln1"), ("fc1", "ln2")):
                     wf, bf, sf = fold_layernorm(w[f"{i}.{mat}.w"], w[f"{i}.{mat}.b"], w[f"{i}.{ln}.w"], w[f"{i}.{ln}.b"])

@@ -68,14 +68,19 @@ def generate_captions(model, images, decode: Optional[Callable[[List[int]], str]
         pv = images if images.dim() == 4 else images.unsqueeze(0)
     else:
         pv = model.image_processor(images=list(images), return_tensors="pt")["pixel_values"]
-    # pixel values on the device once: each batch's encoder then runs beside the previous batch's token
-    # steps (generate_batch next_images), which recognises the very same tensor on the next call
-    pv = pv.to(model.device).float()
-    chunks = [pv[i:i + batch_size] for i in range(0, pv.shape[0], batch_size)]
+    # at most two batches on the device: the current one and the next, whose encoder runs beside this
+    # batch's token steps (generate_batch next_images); the next iteration passes that very tensor object,
+    # which generate_batch recognises as prefetched
+    starts = list(range(0, pv.shape[0], batch_size))
+
+    def dev(i):
+        return pv[i:i + batch_size].to(model.device).float()
     out = []
-    for j, chunk in enumerate(chunks):
-        nxt = chunks[j + 1] if j + 1 < len(chunks) else None
+    chunk = dev(starts[0]) if starts else None
+    for j in range(len(starts)):
+        nxt = dev(starts[j + 1]) if j + 1 < len(starts) else None
         ids = model.generate_batch(chunk, start_token_id, end_token_id, max_len=max_len, next_images=nxt)
+        chunk = nxt
         for seq in ids:
             p = postprocess_ids(seq, start_token_id, end_token_id)
             out.append((p, clean_text(decode(p)) if decode is not None else None))

@@ -82,6 +82,7 @@ class ImageToTextModel:
         self.memory_mode = memory_mode or config.MEMORY_MODE
         if self.memory_mode not in ("cls", "patches"):
             raise ValueError(f"memory_mode must be 'cls' or 'patches', got {self.memory_mode}")
+        self.encoder.configure_for(self.memory_mode)  # residual-stream precision for this memory (encoder.py)
         self.encoder_output_dim = self.encoder.hidden_size
         self.decoder_embed_dim = decoder_embed_dim
         self.decoder_pad_idx = decoder_pad_idx
@@ -252,8 +253,14 @@ class ImageToTextModel:
         if pf is not None and pf[0].data_ptr() == images.data_ptr() and pf[0].shape == images.shape:
             _, self._enc_slot, (enc_rows, enc_ld, S), ev = pf
             native.HipEvents.wait(native.stream_ptr(), ev)
-            return enc_rows, enc_ld, S
-        return self._encoder_rows(images, self._enc_slot)
+            out = enc_rows, enc_ld, S
+        else:
+            out = self._encoder_rows(images, self._enc_slot)
+        # the slot is being read again: a later prefetch into it must wait for this reader (re-armed by
+        # _train_step once the step's readers are issued; every other caller leaves it unarmed, so the
+        # prefetch waits for everything on the main stream)
+        self._slot_freed[self._enc_slot] = False
+        return out
 
     def _encode_memory(self, images: torch.Tensor, refresh: bool = True):
         """Returns (mem_rows, mem_ld, S, enc_rows, enc_ld): memory [B*S rows of d] and the
@@ -264,7 +271,6 @@ class ImageToTextModel:
         self.store.ensure_shadow(force=refresh)
         self._gen += 1
         enc_rows, enc_ld, S = self._take_encoded(images)
-        self._slot_freed[self._enc_slot] = False  # re-armed by _train_step once this step's readers are issued
         if not self.has_projection:
             return enc_rows, enc_ld, S, enc_rows, enc_ld
         key = (B, S)

@@ -18,6 +18,7 @@ from __future__ import annotations
 import argparse
 import math
 import os
+import sys
 import time
 
 import torch
@@ -69,8 +70,11 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
         raise ValueError("data-parallel training runs the fused step: pass optim.AdamW and the reference criterion")
     total = torch.zeros(1, dtype=torch.float32, device=model.device)
     # failure detection: the index of the first batch whose loss is NaN / inf, tracked on the
-    # device (no per-step sync; the reference's all-PAD rows give NaN, dataset.py:116-130), checked at every
-    # log point and at the end of the epoch
+    # device (no per-step sync; the reference's all-PAD rows give NaN, dataset.py:116-130). Checked at the end
+    # of the epoch and, single-process, at every log point. Data parallel: only at the end of the epoch, which
+    # every rank reaches after the same steps (only rank 0 logs; a mid-epoch raise on one rank would leave the
+    # others blocked in the next step's all-reduce). config.NONFINITE_LOSS = "warn" (default: the reference
+    # trains on through a NaN loss) prints the batch index, "raise" stops with NonFiniteLossError.
     first_bad = torch.full((1,), -1, dtype=torch.int64, device=model.device)
     n = 0
     it = _staged(model, dataloader)
@@ -106,14 +110,15 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, grad_clip_v
         first_bad.copy_(torch.where(bad & (first_bad < 0), torch.full_like(first_bad, i), first_bad))
         n += 1
         if log_interval and (i + 1) % log_interval == 0:
-            _raise_if_bad(first_bad, epoch)
+            if dist is None:
+                _check_finite(first_bad, epoch)
             lv = loss.item()
             print(f"epoch {epoch + 1} batch {i + 1}: loss {lv:.4f} lr {_lr_of(optimizer):.2e}", flush=True)
             if wandb_run:
                 wandb_run.log({"train_batch_loss": lv, "learning_rate": _lr_of(optimizer),
                                "global_step": epoch * max(1, len(dataloader)) + i + 1})
         batch = nxt
-    _raise_if_bad(first_bad, epoch)
+    _check_finite(first_bad, epoch)
     return (total / max(n, 1)).item()
 
 
@@ -121,11 +126,19 @@ class NonFiniteLossError(FloatingPointError):
     """A training batch produced a NaN / inf loss (e.g. a batch whose targets are all PAD)."""
 
 
-def _raise_if_bad(first_bad: torch.Tensor, epoch: int):
+def _check_finite(first_bad: torch.Tensor, epoch: int):
+    """Report the first non-finite batch loss of the epoch: raise (config.NONFINITE_LOSS == "raise") or
+    print it once (the default, "warn": training goes on as the reference's does)."""
     i = int(first_bad.item())
-    if i >= 0:
-        raise NonFiniteLossError(f"epoch {epoch + 1}: non-finite training loss at batch {i + 1} (step index {i}); "
-                                 f"the parameters were updated with it -- check the batch (all-PAD targets give NaN)")
+    if i < 0:
+        return
+    msg = (f"epoch {epoch + 1}: non-finite training loss at batch {i + 1} (step index {i}); "
+           f"the parameters were updated with it -- check the batch (all-PAD targets give NaN)")
+    if str(getattr(config, "NONFINITE_LOSS", "warn")).lower() == "raise":
+        raise NonFiniteLossError(msg)
+    if not getattr(first_bad, "_mit_reported", False):  # once per epoch
+        print("warning: " + msg, file=sys.stderr, flush=True)
+        first_bad._mit_reported = True
 
 
 @torch.no_grad()

@@ -14,7 +14,10 @@ so no bf16 implementation meets 1e-2 absolute; DESIGN.md §6 has the table. Boun
            tensor's norm within 10 %.
   The 24-layer CLIP-L configs (cfg2, cfg3: f32 encoder residual stream) are held tighter: logits
   rel-L2 <= 8e-3, encoder <= 1.3x and worst gradient tensor <= 1.5x the reference's bf16 error
-  (measured round 3: 6.8e-3 / 7.4e-3, 1.00x / 0.98x, 1.05x / 1.22x; profiles/r03_bf16_parity.json)."""
+  (measured round 3: 6.8e-3 / 7.4e-3, 1.00x / 0.98x, 1.05x / 1.22x; profiles/r03_bf16_parity.json).
+  Margin: every fixture's logits rel-L2 <= 1.15x the reference's bf16 error and >= 10 %
+  under the 1e-2 bound (<= 9e-3). Each case's metrics are written to gpurun_out/parity/<case>.json
+  (and printed), so the margin of the tree under test is on record after every GPU run."""
 import json
 import os
 
@@ -43,8 +46,13 @@ def test_bf16_within_reference_bf16_envelope(name):
           f"{r['logits_max_abs']:.3f} ({c['logits_max_abs']:.3f}); enc {r['enc_rel_l2']:.2e} ({c['enc_rel_l2']:.2e}); "
           f"grad rms median {r['grad_rms_median']:.3f} ({c['grad_rms_median']:.3f}) max {r['grad_rms_max']:.3f} "
           f"({c['grad_rms_max']:.3f})")
-    assert r["logits_rel_l2"] <= 1e-2
-    assert r["logits_rel_l2"] <= 1.5 * c["logits_rel_l2"]
+    out = os.path.join(os.path.dirname(FX.GOLDEN), "..", "gpurun_out", "parity")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"{name}.json"), "w") as f:
+        json.dump({"ours": r, "reference_bf16": c,
+                   "logits_ratio": r["logits_rel_l2"] / c["logits_rel_l2"]}, f, indent=1)
+    assert r["logits_rel_l2"] <= 9e-3
+    assert r["logits_rel_l2"] <= 1.15 * c["logits_rel_l2"]
     assert r["logits_max_abs"] <= 1.5 * c["logits_max_abs"]
     assert r["argmax_agree_margin_gt_5e-2"] == 1.0
     assert r["enc_rel_l2"] <= 1.75 * c["enc_rel_l2"]

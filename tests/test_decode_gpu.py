@@ -137,11 +137,13 @@ def test_generate_batch_matches_full_recompute(name):
         assert batch[b] == single, (b, batch[b], single)
 
 
-def test_generate_batch_bf16_consistent_with_full_forward():
+@pytest.mark.parametrize("name", ["tiny_vit_patches", "tiny_vit_v509"])
+def test_generate_batch_bf16_consistent_with_full_forward(name):
     """bf16: every token the KV-cached decode picked is the argmax of the model's full (non-cached)
     forward over the same prefix, except where that forward's top-1/top-2 logit margin is a bf16
-    near-tie (< 3e-2) — the decode path computes the reference's recompute up to rounding."""
-    m, meta, _ = _trained("tiny_vit_patches", torch.bfloat16)
+    near-tie (< 3e-2) — the decode path computes the reference's recompute up to rounding.
+    tiny_vit_v509: a vocabulary that is not a multiple of 8 (the fused head's argmax epilogue)."""
+    m, meta, _ = _trained(name, torch.bfloat16)
     img = FX.inputs(meta, 0)[0]
     imgs = torch.cat([img, img.flip(-1)], 0)
     never = 10 ** 6  # run every caption to max_len
@@ -390,6 +392,26 @@ def test_decode_gemm_argmax_keys_exact():
         assert nf.item() == int((want[1:] == end).sum()) and fin[1].item() == 1
 
 
+@pytest.mark.parametrize("V", [509, 1001, 7])
+def test_decode_gemm_argmax_keys_ragged_vocab(V):
+    """argmax_keys on a vocabulary that is not a multiple of 8 (padded_vocab's case): the head runs on the
+    V real rows and no column >= V can win, even when the weight memory past row V holds larger values."""
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(V)
+    M, K = 70, 128
+    a = torch.randint(-2, 3, (M, K), generator=g).to(dev, torch.bfloat16)
+    wp = torch.randint(-2, 3, (V + 8, K), generator=g).to(dev, torch.bfloat16)
+    wp[V:] = 3  # rows past V: would dominate if they were read as columns
+    w = wp[:V]
+    bias = torch.randint(-4, 5, (V + 8,), generator=g).float().to(dev)
+    bias[V:] = 1e4
+    keys = torch.zeros(M, dtype=torch.int64, device=dev)
+    N.decode_gemm(a, w, bias=bias[:V], argmax_keys=keys)
+    want = (a.double() @ w.double().t() + bias[:V].double()).argmax(1)
+    got = 0xFFFFFFFF - (keys & 0xFFFFFFFF)
+    assert torch.equal(got, want)
+
+
 def test_decode_gemm_argmax_keys_rejects_outputs():
     dev = torch.device("cuda")
     a = torch.zeros(4, 64, device=dev, dtype=torch.bfloat16)
@@ -401,7 +423,7 @@ def test_decode_gemm_argmax_keys_rejects_outputs():
         N.decode_gemm(a, w, act=N.ACT_RELU, argmax_keys=keys)
 
 
-@pytest.mark.parametrize("name", ["tiny_vit_patches", "cfg0_b4_patches"])
+@pytest.mark.parametrize("name", ["tiny_vit_patches", "cfg0_b4_patches", "tiny_vit_v509"])
 def test_fused_decode_step_matches_unfused(name, monkeypatch):
     """bf16: the fused step (LayerNorms folded into the GEMMs, the pick folded into the head) and the
     12-launch-per-layer step pick the same ids token after token on a shared prefix wherever the unfused

@@ -161,10 +161,13 @@ def test_optimizer_state_maps_torch_adamw_format(name):
     assert torch.equal(store.exp_avg, before)
 
 
-def test_train_one_epoch_raises_on_non_finite_loss():
-    """Failure detection: a NaN loss (the reference's all-PAD batch) stops the epoch with
-    the step index instead of training on; the check runs on the device flag at log points / epoch end."""
+@pytest.mark.parametrize("dp", [False, True])
+def test_train_one_epoch_non_finite_loss(dp, monkeypatch, capsys):
+    """Failure detection: a NaN loss (the reference's all-PAD batch) is reported with its step
+    index -- raised with config.NONFINITE_LOSS = "raise", printed once by default (the reference trains on).
+    The check runs on a device flag at log points (single process) and at the end of the epoch."""
     import torch
+    import config
     import train as TR
 
     class Tiny(torch.nn.Module):
@@ -187,6 +190,54 @@ def test_train_one_epoch_raises_on_non_finite_loss():
     batches = [{"images": torch.randn(2, 4), "decoder_input_tokens": torch.ones(2, 3, dtype=torch.int64),
                 "target_tokens": torch.randint(1, 5, (2, 3)) if i != 2 else torch.zeros(2, 3, dtype=torch.int64)}
                for i in range(4)]
+    monkeypatch.setattr(config, "NONFINITE_LOSS", "raise")
     with pytest.raises(TR.NonFiniteLossError, match="batch 3 .step index 2"):
-        TR.train_one_epoch(m, batches, opt, crit, "cpu", 1.0, None, 0, 0, None)
+        TR.train_one_epoch(m, batches, opt, crit, "cpu", 1.0, None, 0, 2, None)
     assert TR.train_one_epoch(m, batches[:2], opt, crit, "cpu", 1.0, None, 0, 0, None) > 0
+    monkeypatch.setattr(config, "NONFINITE_LOSS", "warn")
+    capsys.readouterr()
+    TR.train_one_epoch(m, batches, opt, crit, "cpu", 1.0, None, 0, 1, None)
+    err = capsys.readouterr().err
+    assert err.count("non-finite training loss at batch 3 (step index 2)") == 1
+    if dp:  # data parallel: no mid-epoch check (only rank 0 logs), the end-of-epoch one on every rank
+        calls = []
+        monkeypatch.setattr(TR, "_check_finite", lambda fb, ep: calls.append(int(fb.item())))
+        monkeypatch.setattr(TR, "_fused_loss_ok", lambda *a: True)
+
+        class FakeAdamW(TR.optim.AdamW):
+            param_groups = [{"lr": 0.1}]
+
+            def __init__(self):
+                pass
+
+            def zero_grad(self):
+                pass
+
+            def step(self, clip=0.0):
+                pass
+
+        m.train_step = lambda im, di, tg, dist=None, next_images=None: crit(m(im, di), tg).reshape(1)
+        TR.train_one_epoch(m, batches, FakeAdamW(), crit, "cpu", 1.0, None, 0, 1, None, dist=object())
+        assert calls == [2]
+
+
+def test_encoder_residual_stream_policy(monkeypatch):
+    """config.ENCODER_F32_RESIDUAL "auto": the f32 residual stream for the 24-layer CLIP-L towers and for
+    "cls" memory (one encoder row per image reaches the logits undamped, tools/bf16_bisect.py); the folded
+    bf16 stream for ViT towers feeding patch memory (the bench path); fp32 compute never folds."""
+    import torch
+    import config
+    from encoder import VisionEncoder
+    monkeypatch.setattr(config, "ENCODER_F32_RESIDUAL", "auto")
+    vit, clip_l = config.ENCODER_SPECS["google/vit-base-patch16-224-in21k"], config.ENCODER_SPECS[
+        "openai/clip-vit-large-patch14-336"]
+    e = VisionEncoder(vit, torch.device("cpu"), torch.bfloat16)
+    assert (e.res32, e.fold_ln) == (False, True)
+    assert (e.configure_for("cls").res32, e.fold_ln) == (True, False)
+    assert (e.configure_for("patches").res32, e.fold_ln) == (False, True)
+    c = VisionEncoder(clip_l, torch.device("cpu"), torch.bfloat16)
+    assert (c.configure_for("patches").res32, c.fold_ln) == (True, False)
+    f = VisionEncoder(vit, torch.device("cpu"), torch.float32)
+    assert (f.configure_for("cls").res32, f.fold_ln) == (False, False)
+    monkeypatch.setattr(config, "ENCODER_F32_RESIDUAL", "off")
+    assert (e.configure_for("cls").res32, e.fold_ln) == (False, True)
