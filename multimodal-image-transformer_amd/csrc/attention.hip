@@ -12,8 +12,6 @@
 //     Used for fp32 parity mode and for the decoder backward.
 //   * attn_fwd_mfma (bf16): 64-query block per 4-wave workgroup, v_mfma_f32_16x16x32_bf16 for
 //     Q K^T and P V with online softmax over 64-key tiles staged in LDS.
-#include <stdlib.h>
-
 #include "common.h"
 
 namespace {
