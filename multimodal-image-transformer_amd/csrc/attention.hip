@@ -1079,18 +1079,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
       }
     }
     bf16x4 bp4[4], bs4[4];  // (P o M) and dS, 4 consecutive queries (t) per 16-query block nb
+    const bool kdead = !klive || kpad;
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
+      // the 4 queries' log-sum-exp and delta in one 16-B LDS read each (were 8 ds_read_b32)
+      const f32x4 lq4 = *(const f32x4*)(Ls + nb * 16 + g * 4), dl4 = *(const f32x4*)(Dl + nb * 16 + g * 4);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int qq = nb * 16 + g * 4 + t;
-        const bool msk = !klive || kpad || qq >= Lq || (a.causal && kl > qq);
-        const float p = msk ? 0.f : exp2f(s[nb][t] * sl2 - Ls[qq]);
+        const bool msk = kdead || qq >= Lq || (a.causal && kl > qq);
+        // branch-free: v_exp_f32 for every element, the mask selects (ocml's exp2f added a denormal-range
+        // rescale per element, and the masked form compiled into exec-masked branches)
+        const float e = __builtin_amdgcn_exp2f(s[nb][t] * sl2 - lq4[t]);
+        const float p = msk ? 0.f : e;
         const float mul =
             a.dropout ? drop_mul(key, ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qq) * (uint64_t)Lk + kl, a.thresh, a.dscale)
                       : 1.f;
         bp4[nb][t] = (bf16)(p * mul);
-        bs4[nb][t] = (bf16)(p * (dp[nb][t] * mul - Dl[qq]));
+        bs4[nb][t] = (bf16)(p * (dp[nb][t] * mul - dl4[t]));
       }
       // dS^T row kloc, queries nb*16+4g .. +4: 8 bytes in the K-tile swizzle
       *(bf16x4*)(St + koff_k(kloc, nb * 2 + (g >> 1)) + (g & 1) * 8) = bs4[nb];

@@ -43,9 +43,14 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
 // wave-uniform word (scalar work), the index's high half (0 below 2^32 elements) is added before the
 // round. Was two rounds (the second mixing the high halves): the decoder's dropout sites hash every
 // element they touch, forward and backward, so the round is VALU on the critical kernels.
+// The index's high half enters by a rotate-add, not a multiply: v_mul_lo_u32 is a quarter-rate VALU op and
+// every index below 2^32 (all of the train step's) has a zero high half, so the masks are the ones the
+// multiply form gave, bit for bit, at one multiply less per element (the attention backward hashes every
+// score it touches).
 __device__ __forceinline__ uint32_t mix_u32(uint64_t key, uint64_t idx) {
   const uint32_t k = (uint32_t)key ^ ((uint32_t)(key >> 32) * 0x9E3779B9u);
-  return lowbias32(((uint32_t)idx ^ k) + (uint32_t)(idx >> 32) * 0x85EBCA6Bu);
+  const uint32_t hi = (uint32_t)(idx >> 32);
+  return lowbias32(((uint32_t)idx ^ k) + ((hi << 16) | (hi >> 16)));
 }
 __device__ __forceinline__ uint64_t site_key(const uint64_t* seed, uint32_t site) {
   return (seed ? *seed : 0ull) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(site + 1));

@@ -1,7 +1,8 @@
 """Per-shape GEMM time: mit_gemm (our kernels) vs torch.matmul (hipBLASLt, the vendor library as a
 known-good reference on the same device; guide §5.4 rule 10), bf16, random operands, interleaved
 rounds in one process. Shapes = the configs[1] train step's GEMMs (encoder B*197 = 12608 rows,
-decoder B*T = 4032 rows). Usage (GPU box): python tools/blas_reference.py"""
+decoder B*T = 4032 rows); --clip336: the configs[2] step's CLIP-L/14@336 shapes.
+Usage (GPU box): python tools/blas_reference.py [--clip336]"""
 import os
 import sys
 
@@ -30,6 +31,17 @@ SHAPES = [
     ("dec1 fc_out", 256, 10000, 512, 0, 0, 1),
     ("4096^3", 4096, 4096, 4096, 0, 0, 0),
 ]
+# configs[2]: CLIP ViT-L/14@336 (577 tokens, E = 1024, mlp 4096, 24 layers; f32 residual stream, so the
+# o-proj / fc2 GEMMs write the bf16 sublayer output with a bias and no residual) + the 6L d512 decoder with
+# S = 577 memory rows (B * S = 36928)
+CLIP_SHAPES = [
+    ("clip qkv+bias", 36928, 3072, 1024, 0, 0, 24), ("clip o+bias", 36928, 1024, 1024, 0, 0, 24),
+    ("clip fc1+qgelu", 36928, 4096, 1024, 0, 0, 24), ("clip fc2+bias", 36928, 1024, 4096, 0, 0, 24),
+    ("clip patch", 36864, 1024, 592, 0, 0, 1),
+    ("proj 1024->512", 36928, 512, 1024, 0, 0, 1), ("dec kv_all577", 36928, 6144, 512, 0, 0, 1),
+    ("dX kv_all577", 36928, 512, 6144, 0, 1, 1), ("dW kv_all577", 6144, 512, 36928, 1, 1, 1),
+    ("dW proj577", 512, 1024, 36928, 1, 1, 1),
+]
 
 
 def timeit(fn, iters=20):
@@ -51,7 +63,8 @@ def main():
     torch.manual_seed(0)
     tot_ours = tot_blas = 0.0
     print(f"{'shape':14s} {'M':>6s} {'N':>6s} {'K':>6s}  {'ours us':>8s} {'TF':>6s}  {'hipBLASLt us':>12s} {'TF':>6s}  ratio")
-    for name, M, N, K, al, bl, cnt in SHAPES:
+    shapes = CLIP_SHAPES if "--clip336" in sys.argv else SHAPES
+    for name, M, N, K, al, bl, cnt in shapes:
         A = (torch.randn(M, K) if al == 0 else torch.randn(K, M)).to(dev, torch.bfloat16)
         B = (torch.randn(N, K) if bl == 0 else torch.randn(K, N)).to(dev, torch.bfloat16)
         out_f32 = al == 1
@@ -60,8 +73,12 @@ def main():
         kw = {}
         if "res" in name:
             kw["residual"] = torch.randn(M, N, device=dev).to(torch.bfloat16)
-        if "gelu" in name:
+        if "qgelu" in name:
+            kw["act"] = native.ACT_QUICK_GELU
+        elif "gelu" in name:
             kw["act"] = native.ACT_GELU
+        if "bias" in name or "qgelu" in name:
+            kw["bias"] = torch.randn(N, device=dev)
         ours = lambda: native.gemm(A, B, C, M, N, K, a_layout=al, b_layout=bl, workspace=ws, **kw)  # noqa: E731
         At = A if al == 0 else A.t()
         Bt = B.t() if bl == 0 else B
