@@ -317,8 +317,11 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
   }
   const float sl2 = a.scale * 1.4426950408889634f;  // scores in log2 units
   const uint64_t key = a.dropout ? site_key(a.seed, a.site) : 0ull;
-  const uint64_t rowbase = ((uint64_t)(b * H + h) * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
+  // dropout index (bh * Lq + qi) * Lk + key < 2^32 (host-checked): 32-bit, drop_mul32
+  const uint32_t rowbase = ((uint32_t)(b * H + h) * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk + (uint32_t)(g * 4);
+  const uint32_t kf = key_fold(key);
   const int64_t* tok = a.tok ? a.tok + b * a.tok_batch : nullptr;
+  const int qi32 = (int)qi;
 
   long kend = Lk;
   if (a.causal) kend = min(Lk, min(Lq, qblk + AQ));  // keys beyond the block's last query are masked
@@ -377,15 +380,23 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
         st[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kv), qf[kk], st[nb], 0, 0, 0);
       }
     // ---- mask + online softmax (per query = per lane&15) ----
+    // the tile's live keys (in range, not PAD) as one wave ballot: lane l tests key j0 + l (one token load
+    // per lane instead of 16 per-element loads behind branches)
+    uint64_t live;
+    {
+      const long kj = j0 + lane;
+      bool ok = kj < Lk;
+      if (ok && tok) ok = tok[kj] != a.pad;
+      live = __ballot(ok);
+    }
     float s[16];
     float tmax = -INFINITY;
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const long kj = j0 + nb * 16 + g * 4 + t;
-        bool msk = kj >= Lk || (a.causal && kj > qi);
-        if (!msk && tok) msk = tok[kj] == a.pad;
+        const int kb = nb * 16 + g * 4 + t;
+        const bool msk = !((live >> kb) & 1ull) | ((a.causal != 0) & ((int)j0 + kb > qi32));
         const float v = msk ? -INFINITY : st[nb][t] * sl2;
         s[nb * 4 + t] = v;
         tmax = fmaxf(tmax, v);
@@ -393,12 +404,12 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(m, tmax);
-    const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m - mnew);
+    const float alpha = (mnew == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
     float psum = 0.f;
     float p[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      p[k] = (s[k] == -INFINITY) ? 0.f : exp2f(s[k] - mnew);
+      p[k] = (s[k] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(s[k] - mnew);
       psum += p[k];
     }
     psum += __shfl_xor(psum, 16, 64);
@@ -410,7 +421,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(long H, long Lq, long Lk, A
       for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-          p[nb * 4 + t] *= drop_mul(key, rowbase + (uint64_t)(j0 + nb * 16 + g * 4 + t), a.thresh, a.dscale);
+          p[nb * 4 + t] *= drop_mul32(kf, rowbase + (uint32_t)(j0 + nb * 16 + t), a.thresh, a.dscale);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) ot[i] *= alpha;
@@ -555,7 +566,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
         qf[kk] = __builtin_bit_cast(bf16x8, v);
       }
     }
-    const uint64_t rowbase = ((uint64_t)(b * H + h) * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
+    // dropout index (bh * Lq + qi) * Lk + key < 2^32 (host-checked for the DROP instance): 32-bit, drop_mul32
+    const uint32_t rowbase = ((uint32_t)(b * H + h) * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk + (uint32_t)(g * 4);
+    const uint32_t kf = key_fold(key);
     f32x4 ot[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) ot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -628,7 +641,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
         for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
           for (int t = 0; t < 4; ++t)
-            p[nb * 4 + t] *= drop_mul(key, rowbase + (uint64_t)(j0 + nb * 16 + g * 4 + t), a.thresh, a.dscale);
+            p[nb * 4 + t] *= drop_mul32(kf, rowbase + (uint32_t)(j0 + nb * 16 + t), a.thresh, a.dscale);
       }
       // ---- O^T += V^T P^T, two 32-key halves ----
 #pragma unroll
@@ -683,7 +696,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) v
 #pragma unroll
           for (int t = 0; t < 4; ++t)
             if (nb < ntail)
-              p[nb * 4 + t] *= drop_mul(key, rowbase + (uint64_t)(j0 + nb * 16 + g * 4 + t), a.thresh, a.dscale);
+              p[nb * 4 + t] *= drop_mul32(kf, rowbase + (uint32_t)(j0 + nb * 16 + t), a.thresh, a.dscale);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) ot[i] *= alpha;
@@ -1080,6 +1093,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
     }
     bf16x4 bp4[4], bs4[4];  // (P o M) and dS, 4 consecutive queries (t) per 16-query block nb
     const bool kdead = !klive || kpad;
+    // dropout index (bh * Lq + qq) * Lk + kl < 2^32 (host-checked): the lane's part once, then a wave-uniform
+    // step per (nb, t); drop_mul32 hashes it exactly as drop_mul does
+    const uint32_t ilane = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)(g * 4)) * (uint32_t)Lk + (uint32_t)kl;
+    const uint32_t kf = key_fold(key);
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       // the 4 queries' log-sum-exp and delta in one 16-B LDS read each (were 8 ds_read_b32)
@@ -1087,14 +1104,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void a
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int qq = nb * 16 + g * 4 + t;
-        const bool msk = kdead || qq >= Lq || (a.causal && kl > qq);
+        // bitwise, 32-bit: a short-circuit || over 64-bit compares compiled into exec-masked branches
+        const bool msk = kdead | (qq >= (int)Lq) | ((a.causal != 0) & (kloc > qq));
         // branch-free: v_exp_f32 for every element, the mask selects (ocml's exp2f added a denormal-range
         // rescale per element, and the masked form compiled into exec-masked branches)
         const float e = __builtin_amdgcn_exp2f(s[nb][t] * sl2 - lq4[t]);
         const float p = msk ? 0.f : e;
         const float mul =
-            a.dropout ? drop_mul(key, ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qq) * (uint64_t)Lk + kl, a.thresh, a.dscale)
-                      : 1.f;
+            a.dropout ? drop_mul32(kf, ilane + (uint32_t)(nb * 16 + t) * (uint32_t)Lk, a.thresh, a.dscale) : 1.f;
         bp4[nb][t] = (bf16)(p * mul);
         bs4[nb][t] = (bf16)(p * (dp[nb][t] * mul - dl4[t]));
       }
@@ -1198,7 +1215,8 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
   if (mfma_ok) {
     const long kb = 2 * ((Lk - 1) * x->k_row + D), vb = 2 * ((Lk - 1) * x->v_row + D);
     MIT_CHECK_ARG(kb < (1L << 31) && vb < (1L << 31), "mit_attention_fwd: K/V span >= 2 GiB");
-    if (!a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535) {
+    if (!a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535 &&
+        (!a.dropout || (double)B * (double)H * (double)Lq * (double)Lk < 4294967296.0)) {
       // head-resident K/V: one workgroup per (b, h), NW waves balanced over the 16-query tiles.
       // K/V rows are staged to a multiple of 16 (the key tail of < 64 runs 16-key tiles: a ViT-B/16
       // head of 197 keys sweeps 208 instead of 256; 28.5 -> 27.7 us, tools/attn_bench.py). <= 8 waves
@@ -1226,8 +1244,10 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
         hipLaunchKernelGGL(attn_fwd_head<true>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
       else
         hipLaunchKernelGGL(attn_fwd_head<false>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
-    } else {
+    } else if (!a.dropout || (double)B * (double)H * (double)Lq * (double)Lk < 4294967296.0) {
       hipLaunchKernelGGL(attn_fwd_mfma, grid, dim3(256), 0, s, H, Lq, Lk, a, (int)kb, (int)vb);
+    } else {  // dropout indices past 2^32 (the MFMA kernels form them in 32 bits)
+      hipLaunchKernelGGL((attn_fwd_simple<bf16, 64>), grid, dim3(64), 0, s, H, Lq, Lk, a);
     }
   } else if (dtype == MIT_BF16) {
     DISPATCH_DH(Dh, hipLaunchKernelGGL((attn_fwd_simple<bf16, DH>), grid, dim3(64), 0, s, H, Lq, Lk, a));
@@ -1272,7 +1292,9 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
     nb.k = (int)kb;
     nb.v = (int)vb;
     nb.dO = (int)db;
-    if (Lq <= 64 && Lk <= HB_MAXK && H <= 65535 && B <= 65535 && x->o_row % 8 == 0) {
+    // (the head kernel forms its dropout indices in 32 bits: B * H * Lq * Lk < 2^32)
+    if (Lq <= 64 && Lk <= HB_MAXK && H <= 65535 && B <= 65535 && x->o_row % 8 == 0 &&
+        (double)B * (double)H * (double)Lq * (double)Lk < 4294967296.0) {
       const int lkp = (int)((Lk + 31) / 32 * 32);
       const int lds = 2 * lkp * 128 + 2 * 64 * 128 + 2 * 64 * 4;
       static bool attr = false;

@@ -52,6 +52,11 @@ __device__ __forceinline__ uint32_t mix_u32(uint64_t key, uint64_t idx) {
   const uint32_t hi = (uint32_t)(idx >> 32);
   return lowbias32(((uint32_t)idx ^ k) + ((hi << 16) | (hi >> 16)));
 }
+// mix_u32 for an index below 2^32, with the key folded once per thread (key_fold): the same value
+__device__ __forceinline__ uint32_t key_fold(uint64_t key) { return (uint32_t)key ^ ((uint32_t)(key >> 32) * 0x9E3779B9u); }
+__device__ __forceinline__ float drop_mul32(uint32_t kf, uint32_t idx, uint32_t thresh, float scale) {
+  return lowbias32(idx ^ kf) >= thresh ? scale : 0.0f;
+}
 __device__ __forceinline__ uint64_t site_key(const uint64_t* seed, uint32_t site) {
   return (seed ? *seed : 0ull) ^ (0xD6E8FEB86659FD93ull * (uint64_t)(site + 1));
 }
