@@ -110,3 +110,76 @@ def test_bench_size_prefetch_is_bitwise_neutral():
     for losses, master in res[1:]:
         assert losses == res[0][0], (losses, res[0][0])
         assert torch.equal(master, res[0][1])
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_bench_size_step_matches_oracle(dtype):
+    """The benchmarked configuration itself (configs[1]: ViT-B/16 + 6L d512 decoder, patches memory, BATCH 64,
+    seq_len 64 -- the fixtures pin B = 2) against the CPU oracle (oracle/ref_cpu.py, pinned to the reference by
+    tests/test_oracle.py) on the same random-init weights and synthetic batch, dropout off: logits of 8 sampled
+    positions, the step's loss, the pre-clip gradient norm and every post-clip gradient (rel-L2 over all
+    trainable tensors). fp32 mode to the north star's 1e-3; bf16 (the timed path) to its 1e-2 relative logits
+    bound and the bf16 gradient error level of the fixtures."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    sys.path.insert(0, os.path.join(ROOT, "multimodal-image-transformer_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import config
+    import optim
+    from decoder import flat_to_reference
+    from model import ImageToTextModel
+    from oracle import ref_cpu as R
+    bench, a = _bench_args()
+    torch.cuda.set_device(0)
+    config.MEMORY_MODE, config.ENCODER_MODEL_NAME = "patches", "google/vit-base-patch16-224-in21k"
+    m = ImageToTextModel(a.vocab, 512, 8, 6, 2048, 100, 0.0, 0, memory_mode="patches", dtype=dtype, seed=42)
+    opt = optim.AdamW(m.store, lr=1e-4, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-5)
+    dev = torch.device("cuda", 0)
+    images, di, tg = bench.synthetic_batch(a.batch, a.seq_len, a.vocab, dev, 1000, m.encoder.image)
+    sd = {k: v.float().cpu() for k, v in m.state_dict().items()}
+    enc = {"kind": "vit", "heads": 12, "layers": 12, "patch": 16, "eps": 1e-12}
+    dec = {"heads": 8, "layers": 6, "max_seq_len": 100}
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    # forward logits at 8 positions
+    m.eval()
+    with torch.no_grad():
+        logits = m(images, di).float().cpu()
+    m.train()
+    ic, dic, tgc = images.cpu(), di.cpu(), tg.cpu()
+    with torch.no_grad():
+        ref_logits = R.model_forward(sd, ic, dic, enc, dec, "patches")
+    sel = [(0, 0), (5, 17), (17, 62), (31, 1), (40, 33), (47, 50), (55, 9), (63, 61)]
+    got = torch.stack([logits[b, t] for b, t in sel])
+    ref = torch.stack([ref_logits[b, t] for b, t in sel])
+    rel = float((got - ref).norm() / ref.norm())
+    # one train step (train.py:75-100) on both
+    names = [k for k in sd if not k.startswith("encoder.") and not k.endswith("positional_encoding.pe")]
+    ropt = R.AdamWState({k: sd[k] for k in names})
+    rloss, rtotal, rgrads = R.train_step(sd, names, ropt, ic, dic, tgc, enc, dec, "patches", 5.0)
+    loss = m.train_step(images, di, tg).item()
+    opt.step(5.0)
+    total, coef = opt.norm_t.tolist()
+
+    class GV:
+        vocab = m.decoder.V
+
+        def p(self, n):
+            return m.store.g(n)
+    grads = flat_to_reference(GV(), 6, 512)
+    grads["projection.weight"] = m.store.g("projection.weight")
+    grads["projection.bias"] = m.store.g("projection.bias")
+    num = sum(float(((grads[k].float().cpu() * coef) - rgrads[k]).norm() ** 2) for k in names) ** 0.5
+    den = sum(float(rgrads[k].norm() ** 2) for k in names) ** 0.5
+    grel = num / den
+    print(f"{dtype} B=64: logits rel-L2 {rel:.2e}, loss {loss:.6f} vs {rloss:.6f}, grad norm {total:.5f} vs "
+          f"{rtotal:.5f}, post-clip gradient rel-L2 {grel:.2e}")
+    if dtype == "fp32":
+        assert (got - ref).abs().max().item() <= 1e-3
+        assert abs(loss - rloss) <= 1e-4 * abs(rloss)
+        assert abs(total - rtotal) <= 1e-3 * rtotal
+        assert grel <= 1e-3
+    else:
+        assert rel <= 1e-2
+        assert abs(loss - rloss) <= 5e-3
+        assert abs(total - rtotal) <= 1e-2 * rtotal
+        assert grel <= 0.1
