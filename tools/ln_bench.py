@@ -46,6 +46,33 @@ def run(iters=50):
             print(f"{'  copy':22s} {R:6d} x {C:5d}  {t * 1e6:7.2f} us  {nb / t / 1e12:5.2f} TB/s", flush=True)
 
 
+def run_bwd(iters=50):
+    """mit_layernorm_bwd on the decoder's post-LN shape (4032 x 512, residual dropout, dr written, dgamma /
+    dbeta partials left for the side stream): us and TB/s of dy, z read + dx, dr written."""
+    dev = torch.device("cuda")
+    R, C = 4032, 512
+    dy = torch.randn(R, C, device=dev).to(torch.bfloat16)
+    z = torch.randn(R, C, device=dev).to(torch.bfloat16)
+    dx, dr = torch.empty_like(dy), torch.empty_like(dy)
+    mean, rstd = z.float().mean(1), z.float().var(1).add(1e-5).rsqrt()
+    g = torch.randn(C, device=dev)
+    ws = torch.empty(native.layernorm_bwd_ws_floats(R, C), device=dev)
+    seed = torch.tensor([5], dtype=torch.int64, device=dev)
+    fn = lambda: native.layernorm_bwd(dy, z, mean, rstd, g, dx, None, None, ws, dr=dr, drop_p=0.1, seed=seed, site=3)  # noqa: E731
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / iters * 1e-3
+    print(f"{'dec ln bwd 512 +drop':22s} {R:6d} x {C:5d}  {t * 1e6:7.2f} us  {R * C * 8 / t / 1e12:5.2f} TB/s", flush=True)
+
+
 if __name__ == "__main__":
     native.load_library()
     run()
+    run_bwd()
