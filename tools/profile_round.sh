@@ -25,7 +25,7 @@ timeout -s KILL 300 $P --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYC
 f() { find $OUT/$1 -name "$2" | head -n 1; }
 mkdir -p $OUT/keep &&
 python3 tools/rocpd_summary.py --trace $(f trace '*results.db') --fetch $(f fetch '*results.db') \
-  --write $(f write '*results.db') --sq $(f sq '*results.db') --trace-csv $(f trace '*kernel_trace.csv') --bench-json $OUT/trace.json \
+  --write $(f write '*results.db') --sq $(f sq '*results.db') --trace-csv $(f trace '*kernel_trace.csv') --bench-json $OUT/trace.json $( [ -f gpurun_out/bench_$TAG.json ] && echo --bench-plain gpurun_out/bench_$TAG.json ) \
   --command "rocprofv3 --kernel-trace --stats / --pmc FETCH_SIZE / --pmc WRITE_SIZE / --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -- python3 bench.py $ARGS" \
   --out $OUT/keep/$TAG > $OUT/keep/summary.txt &&
 cp $(f trace '*kernel_stats.csv') $OUT/keep/${TAG}_bench_kernel_stats.csv &&

@@ -86,7 +86,8 @@ def main():
                     "SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE)")
     ap.add_argument("--trace-csv", default=None, help="kernel trace CSV of the same run: the GEMM launches of "
                     "bench.py's roofline replay (after the last AdamW) averaged per (kernel, a_layout, b_layout)")
-    ap.add_argument("--bench-json", default=None, help="bench.py output line to cross-check")
+    ap.add_argument("--bench-json", default=None, help="bench.py output line of the traced run")
+    ap.add_argument("--bench-plain", default=None, help="bench.py output line of an un-profiled run of the same command")
     a = ap.parse_args()
     if a.trace_csv:
         import collections
@@ -110,14 +111,35 @@ def main():
                 return None
             t = v[len(v) // 4:]
             return round((t[-1][1] - t[0][0]) / len(t) / 1e3, 2)
-        chk = {"source": "rocprofv3 --kernel-trace of bench.py: the roofline replay launches (after the last AdamW)",
-               "avg_us_trace": {k: round(sum(v) / len(v) / 1e3, 2) for k, v in sorted(d.items())},
-               "span_per_launch_us_trace": {k: span_per_launch(v) for k, v in sorted(spans.items())},
-               "launches_trace": {k: len(v) for k, v in sorted(d.items())}}
+        # the in-step launches the line's achieved / frac come from: the eager probe steps, each behind a
+        # torch.cuda._sleep spin (spin_kernel), up to the last AdamW
+        first_spin = min((i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]), default=None)
+        ins = collections.defaultdict(list)
+        if first_spin is not None:
+            for r in rows[first_spin:last + 1]:
+                m = re.search(r"(gemm256_kernel|gemm_bf16_kernel)<(\d), (\d)", r["Kernel_Name"])
+                if m:
+                    ins[f"{m.group(1)}<{m.group(2)},{m.group(3)}>"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        chk = {"source": "rocprofv3 --kernel-trace of bench.py",
+               "in_step": {"what": "launches of the eager probe steps (first spin_kernel .. last AdamW): the "
+                                   "launches the line's roofline.avg_launch_us times with HIP event pairs",
+                           "avg_us_trace": {k: round(sum(v) / len(v) / 1e3, 2) for k, v in sorted(ins.items())},
+                           "launches_trace": {k: len(v) for k, v in sorted(ins.items())}},
+               "replay": {"what": "the roofline replay launches (after the last AdamW): avg_launch_us_isolated_replay",
+                          "avg_us_trace": {k: round(sum(v) / len(v) / 1e3, 2) for k, v in sorted(d.items())},
+                          "span_per_launch_us_trace": {k: span_per_launch(v) for k, v in sorted(spans.items())},
+                          "launches_trace": {k: len(v) for k, v in sorted(d.items())}}}
         if a.bench_json:
             line = [x for x in open(a.bench_json) if x.startswith("{")][-1]
             rf = json.loads(line).get("roofline", {})
-            chk["bench_roofline"] = {"kernel": rf.get("kernel"), "avg_launch_us": rf.get("avg_launch_us")}
+            chk["bench_roofline_under_profiler"] = {"kernel": rf.get("kernel"), "avg_launch_us": rf.get("avg_launch_us"),
+                                                    "avg_launch_us_isolated_replay": rf.get("avg_launch_us_isolated_replay")}
+        if a.bench_plain:
+            line = [x for x in open(a.bench_plain) if x.startswith("{")][-1]
+            rf = json.loads(line).get("roofline", {})
+            chk["bench_roofline_plain"] = {"kernel": rf.get("kernel"), "avg_launch_us": rf.get("avg_launch_us"),
+                                           "frac": rf.get("frac"),
+                                           "avg_launch_us_isolated_replay": rf.get("avg_launch_us_isolated_replay")}
         with open(a.out + "_roofline_check.json", "w") as f:
             json.dump(chk, f, indent=1)
         print(json.dumps(chk))
