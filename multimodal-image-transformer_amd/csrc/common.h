@@ -108,41 +108,37 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
-// GELU (erf form) without ocml's branchy erff, for bf16 epilogues: Phi(x) = 1 - 0.5*erfc(x/sqrt2)
-// with erfc(a) = t*P(t)*exp(-a^2), t = 1/(1 + 0.3275911 a) (Abramowitz-Stegun 7.1.26, |error| of
-// erf <= 1.5e-7), evaluated on |x| so the negative tail keeps its relative accuracy (no 1 - 1).
-// ~12 VALU ops incl. one v_rcp and one v_exp; fp32 parity mode keeps gelu_erf.
+// GELU (erf form) for bf16 epilogues with ONE transcendental and no select: x Phi(x) = max(x, 0) - |x| h,
+// h = Phi(-|x|) = 2^q(a), a = min(|x|, 6), q a degree-7 fit of log2 Phi(-a) on [0, 6] (tools/gelu_fit.py):
+// relative error <= 6.6e-6 for |x| <= 6 (1/300 of a bf16 half-ulp; the negative tail keeps its relative
+// accuracy, no 1 - 1), |error| <= 1.2e-8 below -6. 10 VALU + one v_exp_f32, against the A&S 7.1.26
+// form's rcp + exp + compare / select; fp32 parity mode keeps gelu_erf.
+#define MIT_GELU_Q(F) F(-1.834813247e-06f), F(6.159832992e-05f), F(-9.305251297e-04f), F(8.507891558e-03f), \
+                      F(-5.396007001e-02f), F(-4.584643841e-01f), F(-1.151251078e+00f), F(-9.999952912e-01f)
+#define MIT_GELU_S(c) c
 __device__ __forceinline__ float gelu_fast(float x) {
-  const float a = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float h = 0.5f * p * t * __expf(-a * a);  // 0.5 * erfc(|x|/sqrt2) = Phi(-|x|)
-  return x * (x >= 0.0f ? 1.0f - h : h);
+  constexpr float q[8] = {MIT_GELU_Q(MIT_GELU_S)};
+  const float a = fminf(fabsf(x), 6.0f);
+  float p = fmaf(q[0], a, q[1]);
+#pragma unroll
+  for (int k = 2; k < 8; ++k) p = fmaf(p, a, q[k]);
+  return fmaf(-fabsf(x), __builtin_amdgcn_exp2f(p), fmaxf(x, 0.0f));
 }
 
-// gelu_fast on two values with packed FP32 math (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of
-// the polynomial per instruction); the rcp / exp stay scalar. The A&S 7.1.26 evaluation with the
-// constants folded: t = 1 / (1 + (0.3275911/sqrt2)|x|), h = Phi(-|x|) = t * (P(t)/2) * 2^(-x^2 log2(e)/2)
-// (the 0.5 in the coefficients, the exp's log2(e)/2 in one multiply of x^2), y = x >= 0 ? x - x h : x h
-// (enc fc1+GELU 85.3-88.1 vs 88.9-90.3 us with the unfolded form, step +0.25 %).
+// gelu_fast on two values: the polynomial in packed FP32 (v_pk_fma_f32, two values per instruction);
+// min / exp2 / the final max + fma scalar
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
-  const f32x2 ax = __builtin_elementwise_abs(x);
-  const f32x2 d = __builtin_elementwise_fma(f32x2{0.23164189f, 0.23164189f}, ax, f32x2{1.0f, 1.0f});
-  const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
-  f32x2 p = __builtin_elementwise_fma(f32x2{0.5307027145f, 0.5307027145f}, t, f32x2{-0.7265760135f, -0.7265760135f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.7107068705f, 0.7107068705f});
-  p = __builtin_elementwise_fma(p, t, f32x2{-0.142248368f, -0.142248368f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.127414796f, 0.127414796f});
-  const f32x2 z = (x * x) * -0.72134752044448170f;  // -x^2/2 in log2 units
-  const f32x2 e = {__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])};
-  const f32x2 xh = x * (p * t * e);
-  const f32x2 xm = x - xh;
-  return f32x2{x[0] >= 0.0f ? xm[0] : xh[0], x[1] >= 0.0f ? xm[1] : xh[1]};
+  constexpr float q[8] = {MIT_GELU_Q(MIT_GELU_S)};
+  const f32x2 a = {fminf(fabsf(x[0]), 6.0f), fminf(fabsf(x[1]), 6.0f)};
+  f32x2 p = __builtin_elementwise_fma(f32x2{q[0], q[0]}, a, f32x2{q[1], q[1]});
+#pragma unroll
+  for (int k = 2; k < 8; ++k) p = __builtin_elementwise_fma(p, a, f32x2{q[k], q[k]});
+  return f32x2{fmaf(-fabsf(x[0]), __builtin_amdgcn_exp2f(p[0]), fmaxf(x[0], 0.0f)),
+               fmaf(-fabsf(x[1]), __builtin_amdgcn_exp2f(p[1]), fmaxf(x[1], 0.0f))};
 }
+#undef MIT_GELU_S
+#undef MIT_GELU_Q
 
 // Kernel extent asserts (sanitizers): compiled in only by the diagnostic build
 // (`make -C multimodal-image-transformer_amd/csrc asserts` -> lib/variants/libmit_hip_asserts.so, loaded with

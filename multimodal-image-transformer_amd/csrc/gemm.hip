@@ -68,8 +68,8 @@ struct Epi {
 constexpr int ACT_RT = -1;
   // activation read from Epi::act at run time (generic instance)
 
-// FAST: bf16 vector epilogues use the branch-free GELU (gelu_fast, |err| ~1e-7, far below bf16
-// rounding); the scalar / fp32-parity path keeps ocml's erff
+// FAST: bf16 vector epilogues use the one-exp GELU (gelu_fast, relative error <= 6.6e-6, far below
+// bf16 rounding); the scalar / fp32-parity path keeps ocml's erff
 template <int ACT, bool FAST = false>
 __device__ __forceinline__ float act_apply(int rt, float v) {
   const int a = ACT == ACT_RT ? rt : ACT;
