@@ -107,7 +107,41 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+// quick_gelu(x) = x / (1 + e^(-1.702 x)), the form the kernels computed through round 5 (the compiler's
+// IEEE division expansion: v_div_scale / v_div_fmas / v_div_fixup around a denormal-mode switch)
+__device__ __forceinline__ float quick_gelu_ieee(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+// the same quotient for |x| <= 51 without the expansion: v_rcp_f32 of d in [1, 2^126), then one
+// FMA-corrected quotient (Markstein), the sign of x restored for x = -0 (a Newton step on the reciprocal
+// first is not needed: 0 of 2^32 inputs differ without it)
+__device__ __forceinline__ float quick_gelu_core(float x) {
+  const float d = 1.0f + __expf(-1.702f * x);
+  const float y = __builtin_amdgcn_rcpf(d);
+  const float q = x * y;
+  return copysignf(fmaf(fmaf(-d, q, x), y, q), x);
+}
+// N values: the core form for all of them, and ONE branch (no lane of a real activation takes it) back to
+// the division when any |x| > 51 or is not finite (d near or past the float range). Bitwise identical to
+// quick_gelu_ieee over all 2^32 inputs (tools/qgelu_exhaustive.hip); per-value branches cost more than the
+// expansion they save (CLIP fc1 374 vs 343 us)
+template <int N>
+__device__ __forceinline__ void quick_gelu_n(float* v) {
+  float x[N];
+  bool slow = false;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    x[k] = v[k];
+    slow |= !(fabsf(x[k]) <= 51.0f);
+    v[k] = quick_gelu_core(x[k]);
+  }
+  if (__builtin_expect(slow, 0)) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = quick_gelu_ieee(x[k]);
+  }
+}
+__device__ __forceinline__ float quick_gelu(float x) {
+  quick_gelu_n<1>(&x);
+  return x;
+}
 // GELU (erf form) for bf16 epilogues with ONE transcendental and no select: x Phi(x) = max(x, 0) - |x| h,
 // h = Phi(-|x|) = 2^q(a), a = min(|x|, 6), q a degree-7 fit of log2 Phi(-a) on [0, 6] (tools/gelu_fit.py):
 // relative error <= 6.6e-6 for |x| <= 6 (1/300 of a bf16 half-ulp; the negative tail keeps its relative

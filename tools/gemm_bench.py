@@ -24,7 +24,7 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("dW ffn ws", 2048, 512, 4032, 1, 1, "ws"),
     # CLIP ViT-L/14 encoder shapes: configs[2] (336 px, 577 tokens) and configs[3] (224 px, 257)
     ("clip o+res", 36928, 1024, 1024, 0, 0, "res"), ("clip fc2+res", 36928, 1024, 4096, 0, 0, "res"),
-    ("clip qkv", 36928, 3072, 1024, 0, 0, "bias"), ("clip fc1+gelu", 36928, 4096, 1024, 0, 0, "gelu"),
+    ("clip qkv", 36928, 3072, 1024, 0, 0, "bias"), ("clip fc1+gelu", 36928, 4096, 1024, 0, 0, "gelu"), ("clip fc1+qgelu", 36928, 4096, 1024, 0, 0, "qgelu"),
     ("cfg3 o+res", 16448, 1024, 1024, 0, 0, "res"), ("cfg3 fc2+res", 16448, 1024, 4096, 0, 0, "res"),
     # epilogue-concurrency probes (tools/g256_stamps.py): 8 / 64 / 128 tiles of the encoder's K = 768
     ("iso8", 2048, 256, 768, 0, 0), ("iso8 res", 2048, 256, 768, 0, 0, "res"), ("iso64", 2048, 2048, 768, 0, 0),
@@ -55,6 +55,8 @@ def run(iters=20, variants=(1, 2)):
             kw["bias"] = torch.randn(N, device=dev)
         if epi == "gelu":
             kw["act"] = native.ACT_GELU
+        if epi == "qgelu":
+            kw["act"] = native.ACT_QUICK_GELU
         if epi == "res":
             kw["residual"] = torch.randn(M, N, device=dev).to(torch.bfloat16)
         if epi == "reludrop":
