@@ -46,6 +46,28 @@ def run(iters=50):
             print(f"{'  copy':22s} {R:6d} x {C:5d}  {t * 1e6:7.2f} us  {nb / t / 1e12:5.2f} TB/s", flush=True)
 
 
+def run_x32(iters=30):
+    """mit_layernorm_fwd_x32 on the CLIP-L/14@336 residual stream (36928 x 1024: z = x + r in place, f32;
+    y = LN(z) bf16): us and TB/s of x, r read + z, y written (12 B per element)."""
+    dev = torch.device("cuda")
+    R, C = 36928, 1024
+    x = torch.randn(R, C, device=dev)
+    r = torch.randn(R, C, device=dev).to(torch.bfloat16)
+    y = torch.empty(R, C, device=dev, dtype=torch.bfloat16)
+    g, b = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    for _ in range(3):
+        native.layernorm_fwd_x32(x, g, b, 1e-5, y, r=r, z=x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        native.layernorm_fwd_x32(x, g, b, 1e-5, y, r=r, z=x)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / iters * 1e-3
+    print(f"{'clip ln x32 1024 +res':22s} {R:6d} x {C:5d}  {t * 1e6:7.2f} us  {R * C * 12 / t / 1e12:5.2f} TB/s", flush=True)
+
+
 def run_bwd(iters=50):
     """mit_layernorm_bwd on the decoder's post-LN shape (4032 x 512, residual dropout, dr written, dgamma /
     dbeta partials left for the side stream): us and TB/s of dy, z read + dx, dr written."""
@@ -72,7 +94,10 @@ def run_bwd(iters=50):
     print(f"{'dec ln bwd 512 +drop':22s} {R:6d} x {C:5d}  {t * 1e6:7.2f} us  {R * C * 8 / t / 1e12:5.2f} TB/s", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "x32":
+    native.load_library()
+    run_x32()
+elif __name__ == "__main__":
     native.load_library()
     run()
     run_bwd()
