@@ -24,14 +24,16 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, backend="gloo"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.join(here, "..", "multimodal-image-transformer_amd"), os.path.join(here, "golden")):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         import fixtures as FX
         import optim
@@ -64,14 +66,19 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_dp2_train_step_on_hip_path_matches_reference():
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (1, "nccl")])
+def test_dp2_train_step_on_hip_path_matches_reference(world, backend):
+    """world 2 / gloo: the two halves on cuda:0. world 1 / nccl: ONE rank over RCCL (the backend the
+    driver's multi-GPU runs use; this box has one GPU, and RCCL takes one GPU per rank) -- the same
+    DataParallel path with ProcessGroupNCCL: the bucket all-reduces issued under the weight-gradient
+    side stream (decoder._SideStream.under) and joined before clip + AdamW."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     meta, T = FX.load("dp2_tiny")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, backend)) for r in range(world)]
     for p in procs:
         p.start()
     loss, grad, (total, coef), deltas = q.get(timeout=240)
