@@ -477,7 +477,7 @@ def spawn_ranks(args) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)  # 20 steps read ~0.5 % low: the first replay's enqueue latency is timed too
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="pairs per GPU")
     ap.add_argument("--seq-len", type=int, default=64)
