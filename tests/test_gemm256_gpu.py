@@ -79,6 +79,40 @@ def test_gemm256_epilogues():
     assert _rel(out, F.relu(base + bias) * mk.view(M, Nn)) < 8e-3
 
 
+@pytest.mark.parametrize("r", [1, 63, 64, 65, 127, 128, 129, 191, 192, 193, 255])
+def test_gemm256_ragged_last_row_tile(r):
+    """The last row tile with r live rows of 256 (each wave group's 64-row halves live, partly live or
+    dead): every epilogue form against fp32 torch, and nothing written past row M (sentinel rows after
+    the output)."""
+    M, Nn, K = 256 + r, 520, 200
+    N.gemm_set_variant(2)
+    g = torch.Generator().manual_seed(r)
+    x = torch.randn(M, K, generator=g).to(dev(), torch.bfloat16)
+    w = (torch.randn(Nn, K, generator=g) / 10).to(dev(), torch.bfloat16)
+    bias = torch.randn(Nn, generator=g).to(dev())
+    res = torch.randn(M, Nn, generator=g).to(dev(), torch.bfloat16)
+    base = x.float() @ w.float().t()
+    sentinel = -12288.0  # exact in bf16
+
+    def buf(dtype):
+        b = torch.full((M + 64, Nn), sentinel, device=dev(), dtype=dtype)
+        return b, b[:M]
+
+    whole, out = buf(torch.float32)
+    N.gemm(x, w, out, M, Nn, K)
+    assert _rel(out, base) < 1e-5
+    assert (whole[M:] == sentinel).all()
+    for act, fn in [(N.ACT_GELU, F.gelu), (N.ACT_QUICK_GELU, lambda t: t * torch.sigmoid(1.702 * t))]:
+        whole, out = buf(torch.bfloat16)
+        N.linear(x, w, out, bias=bias, act=act)
+        assert _rel(out, fn(base + bias)) < 8e-3
+        assert (whole[M:].float() == sentinel).all()
+    whole, out = buf(torch.bfloat16)
+    N.linear(x, w, out, bias=bias, residual=res)
+    assert _rel(out, base + bias + res.float()) < 8e-3
+    assert (whole[M:].float() == sentinel).all()
+
+
 def test_gemm256_rowsum_weight_grad():
     """dW = dY^T X with the fused bias-gradient row sums (TN layout, f32 out)."""
     R, dout, din = 1032, 520, 264
