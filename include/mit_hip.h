@@ -114,6 +114,11 @@ typedef struct {
    * (the next LayerNorm's ln_stats). Both need bf16 NT operands and a plain bf16 vector epilogue
    * (stats_out: a residual, no activation); they run on the 256x256 tile kernel. */
   float* stats_out;
+  /* tiles: the output tile choice. 0 = per shape (a cost model of this launch's rounds on an otherwise
+   * idle chip); 256 = the 256x256 kernel wherever it applies (bf16 NT, M and N >= 256, no split-K): for a
+   * caller whose other stream runs beside this launch, so a partial last round is not left idle
+   * (encoder.forward_iter_groups); 128 = the 128x128 kernel. mit_gemm_set_variant 1 / 2 / 3 override it. */
+  int tiles;
 } mit_gemm_args;
 int mit_gemm(const mit_gemm_args* args, void* stream);
 long mit_gemm_workspace_bytes(long M, long N, long K);

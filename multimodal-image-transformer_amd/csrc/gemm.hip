@@ -1539,13 +1539,14 @@ bool use_rs(const mit_gemm_args* g) {
 // Occupancy-quantised cost model: the 128x128 kernel runs 2 blocks per CU, the 256x256 kernel 1;
 // a "round" fills every slot once, and a round of the 256 kernel moves 4 tiles' worth of 128x128
 // work per CU-slot at REL256 x the 128 kernel's per-FLOP speed (tools/gemm_bench.py).
-bool use_256(long M, long N, long K, int a_layout) {
+bool use_256(long M, long N, long K, int a_layout, int tiles) {
   const int v = gemm_variant();
   if (v == 1) return false;
   if (v == 2) return true;
   // the MN-contig-A instances (weight gradients) exceed 256 VGPRs and spill: 128 kernel (+ split-K)
   if (a_layout != MIT_K_CONTIG) return false;
-  if (M < 256 || N < 256 || K < 128) return false;
+  if (M < 256 || N < 256 || K < 128 || tiles == 128) return false;
+  if (tiles == 256) return true;  // the caller runs other work beside this launch (mit_gemm_args.tiles)
   const double REL256 = 1.3, CUS = 256.0;
   const double t128 = (double)(((M + 127) / 128) * ((N + 127) / 128));
   const double t256 = (double)(((M + 255) / 256) * ((N + 255) / 256));
@@ -1658,7 +1659,7 @@ extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
   const Split sp = plan_split(g);
   if (ksplit) *ksplit = sp.ks;
   if (sp.ks == 1 && use_rs(g)) return 65;  // the 64x64 register-streaming kernel
-  const bool big = sp.ks == 1 && (use_256(g->M, g->N, g->K, g->a_layout) || g->ln_stats || g->stats_out) &&
+  const bool big = sp.ks == 1 && (use_256(g->M, g->N, g->K, g->a_layout, g->tiles) || g->ln_stats || g->stats_out) &&
                    epi_kind(g) != EK_GENERIC && (g->act == MIT_ACT_NONE || (!g->residual && !g->aux));
   return big ? 256 : 128;
 }
@@ -1737,7 +1738,7 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   if (g->dtype == MIT_BF16) {
     const int ab = (int)a_bytes, bb = (int)b_bytes;
     const Split sp = plan_split(g);
-    const bool big = sp.ks == 1 && (use_256(g->M, g->N, g->K, g->a_layout) || g->ln_stats || g->stats_out);
+    const bool big = sp.ks == 1 && (use_256(g->M, g->N, g->K, g->a_layout, g->tiles) || g->ln_stats || g->stats_out);
     if (g->a_layout == 0 && g->b_layout == 0) launch_layout<0, 0>(g, e, ab, bb, sp, big, s);
     else if (g->a_layout == 0 && g->b_layout == 1) launch_layout<0, 1>(g, e, ab, bb, sp, big, s);
     else if (g->a_layout == 1 && g->b_layout == 0) launch_layout<1, 0>(g, e, ab, bb, sp, big, s);

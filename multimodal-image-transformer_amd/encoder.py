@@ -52,6 +52,9 @@ def _normalize_hf_key(k: str) -> str:
     return k
 
 
+_END = object()  # end-of-generator sentinel (forward_iter_groups)
+
+
 def drain(it):
     """Run a launch-chunk generator (VisionEncoder.forward_iter) to its end; returns its result."""
     while True:
@@ -307,10 +310,13 @@ class VisionEncoder:
         strided view [B, E] of the [B, N, E] buffer (row stride N*E)."""
         return drain(self.forward_iter(images, rows, slot))
 
-    def forward_iter(self, images: torch.Tensor, rows: str = "all", slot: int = 0):
+    def forward_iter(self, images: torch.Tensor, rows: str = "all", slot: int = 0, out: Optional[torch.Tensor] = None,
+                     tiles: int = 0):
         """forward() as a generator of launch chunks: the patch embedding, then one chunk per layer, each
         chunk followed by a yield; the final chunk (last LayerNorm) returns forward()'s result (drain()).
-        The train step issues these chunks between its decoder layers (model.prefetch_encoder_iter)."""
+        The train step issues these chunks between its decoder layers (model.prefetch_encoder_iter).
+        out: [B*N, E] rows the f32-stream forward writes its result into; tiles: the f32-stream GEMMs' tile
+        kernel (mit_gemm_args.tiles; both for forward_iter_groups)."""
         B = images.shape[0]
         if tuple(images.shape[1:]) != (3, self.image, self.image):
             raise ValueError(f"expected images [B,3,{self.image},{self.image}], got {tuple(images.shape)}")
@@ -319,7 +325,9 @@ class VisionEncoder:
         native.im2col(images, ws["cols"], self.patch, self.kpad)
         act = native.ACT_GELU if self.kind == "vit" else native.ACT_QUICK_GELU
         if self.res32:
-            return (yield from self._forward_res32(B, ws, rows, act))
+            return (yield from self._forward_res32(B, ws, rows, act, out, tiles))
+        if out is not None or tiles:
+            raise ValueError("forward_iter: out= / tiles= are for the f32 residual stream")
         native.linear(ws["cols"], w["patch.w"], ws["pt"], bias=w["patch.b"])
         h = ws["h"]
         native.vit_assemble(ws["pt"], w["cls"], w["pos"], h, B, self.np, E)
@@ -334,9 +342,54 @@ class VisionEncoder:
             yield
         return self._finish(B, ws, h, rows)
 
-    def _attention(self, B, a, qkv, o, i):
+    # f32-stream towers of at least this many rows run their prefetched forward as two image groups
+    # (CLIP-L/14@336 at B = 64, 36,928 rows: configs[2] 1879 -> 2010 pairs/s on one box). Not the ViT-B/16
+    # bench path (12,608 rows, folded bf16 stream): its partial rounds already hold the decoder's kernels,
+    # and two groups were 1-2 % slower there (13.0-13.2 k vs 13.3 k pairs/s, profiles/r05_decoder_experiments.txt)
+    GROUP_ROWS = 32768
+
+    def groups_for(self, B: int, rows: str = "all") -> int:
+        """2 when forward_iter_groups applies (CLIP-L/14@336 at B = 64: 36,928 rows), else 1."""
+        return 2 if (self.res32 and rows == "all" and B % 2 == 0 and B * self.N >= self.GROUP_ROWS) else 1
+
+    def forward_iter_groups(self, images: torch.Tensor, slot: int, stream2: "torch.cuda.Stream", events):
+        """forward_iter(images, "all", slot) as two image groups of B / 2, one on the current stream and
+        one on stream2, issued chunk by chunk in lockstep. Every 256-tile GEMM grid ends in a partial
+        round (CLIP-L/14@336, B = 64: fc2 580 tiles = 2.27 rounds of the 256 CUs, fc1 2320 = 9.06): the
+        other group's kernels run in it. Each image goes through the same kernels either way (every op
+        is row- or image-wise); the result is one [B*N, E] buffer. events: a native.HipEvents pool (plan-
+        captured edges); the current stream waits for stream2 before the result is returned."""
+        B = images.shape[0]
+        Bg, N, E = B // 2, self.N, self.E
+        key = ("groups_out", B, slot)
+        if key not in self._ws:
+            self._ws[key] = torch.empty(B * N, E, dtype=self.dtype, device=self.device)
+        gout = self._ws[key]
+        s0, s1 = native.stream_ptr(), stream2.cuda_stream
+        events.wait_stream(s1, s0)  # group 1 starts behind everything issued on the current stream
+        # 256 tiles for every GEMM (per shape, the half-batch o-proj / fc2 would take the 128 kernel, whose
+        # cost model counts the partial round as idle: 31.3 instead of 28.2 ms, tools/enc_groups_bench.py)
+        gens = [self.forward_iter(images[g * Bg:(g + 1) * Bg], "all", 16 + 2 * slot + g,
+                                  out=gout[g * Bg * N:(g + 1) * Bg * N], tiles=256) for g in range(2)]
+        done = [False, False]
+        while True:
+            for g in range(2):
+                if done[g]:
+                    continue
+                if g == 1:
+                    with torch.cuda.stream(stream2):
+                        done[g] = next(gens[g], _END) is _END
+                else:
+                    done[g] = next(gens[g], _END) is _END
+            if all(done):
+                break
+            yield
+        events.wait_stream(s0, s1)
+        return gout.view(B, N, E)
+
+    def _attention(self, B, a, qkv, o, i, tiles=0):
         w, E, N, H = self.w, self.E, self.N, self.H
-        native.linear(a, w[f"{i}.qkv.w"], qkv, bias=w[f"{i}.qkv.b"])
+        native.linear(a, w[f"{i}.qkv.w"], qkv, bias=w[f"{i}.qkv.b"], tiles=tiles)
         args = native.attn_args(qkv, 3 * E, N * 3 * E, qkv[:, E:], 3 * E, N * 3 * E, qkv[:, 2 * E:], 3 * E,
                                 N * 3 * E, o, E, N * E, scale=1.0 / math.sqrt(self.hd))
         native.attention_fwd(native.dtype_code(qkv), B, H, N, N, args, Dh=self.hd)
@@ -374,7 +427,7 @@ class VisionEncoder:
                         ln_colsum=w[f"{i}.fc1.sf"], ln_eps=self.eps)
             native.gemm(m, w[f"{i}.fc2.w"], h, R, E, self.mlp, bias=w[f"{i}.fc2.b"], residual=h, stats_out=st)
 
-    def _forward_res32(self, B, ws, rows, act):
+    def _forward_res32(self, B, ws, rows, act, out=None, tiles=0):
         """The same forward with the residual stream h32 in f32: every sublayer output (o-proj, fc2)
         is written in bf16 to d and added to h32 in f32 by the next LayerNorm (z = h32 + d written back,
         y = LN(z)), so the stream is never rounded to bf16 -- torch.autocast's arithmetic for the
@@ -394,14 +447,15 @@ class VisionEncoder:
         for i in range(self.L):
             native.layernorm_fwd_x32(h32, w[f"{i}.ln1.w"], w[f"{i}.ln1.b"], self.eps, a, r=pend,
                                      z=h32 if pend is not None else None)
-            self._attention(B, a, qkv, o, i)
-            native.linear(o, w[f"{i}.o.w"], d, bias=w[f"{i}.o.b"])
+            self._attention(B, a, qkv, o, i, tiles)
+            native.linear(o, w[f"{i}.o.w"], d, bias=w[f"{i}.o.b"], tiles=tiles)
             native.layernorm_fwd_x32(h32, w[f"{i}.ln2.w"], w[f"{i}.ln2.b"], self.eps, a, r=d, z=h32)
-            native.linear(a, w[f"{i}.fc1.w"], m, bias=w[f"{i}.fc1.b"], act=act)
-            native.linear(m, w[f"{i}.fc2.w"], d, bias=w[f"{i}.fc2.b"])
+            native.linear(a, w[f"{i}.fc1.w"], m, bias=w[f"{i}.fc1.b"], act=act, tiles=tiles)
+            native.linear(m, w[f"{i}.fc2.w"], d, bias=w[f"{i}.fc2.b"], tiles=tiles)
             pend = d
             yield
-        N, out = self.N, ws["out"]
+        N = self.N
+        out = ws["out"] if out is None else out
         if self.kind == "vit":
             if rows == "cls":
                 native.layernorm_fwd_x32(h32, w["final_ln.w"], w["final_ln.b"], self.eps, out, r=pend, rows=B,

@@ -18,7 +18,7 @@ from torch.utils._python_dispatch import TorchDispatchMode
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MIT_HIP_LIB", os.path.join(_HERE, "lib", "libmit_hip.so"))
-ABI_VERSION = 4  # mit_abi_version() of the library this binding matches (include/mit_hip.h)
+ABI_VERSION = 5  # mit_abi_version() of the library this binding matches (include/mit_hip.h)
 
 F32, BF16 = 0, 1
 K_CONTIG, MN_CONTIG = 0, 1
@@ -44,7 +44,7 @@ class GemmArgs(ctypes.Structure):
                 ("bias", vp), ("act", I), ("residual", vp), ("ldr", L), ("aux", vp), ("ld_aux", L),
                 ("aux_scale", Fl), ("drop_p", Fl), ("seed", vp), ("site", U32), ("out_f32", I),
                 ("accumulate", I), ("rowsum", vp), ("workspace", vp), ("workspace_bytes", L),
-                ("ln_stats", vp), ("ln_colsum", vp), ("ln_parts", I), ("ln_eps", Fl), ("stats_out", vp)]
+                ("ln_stats", vp), ("ln_colsum", vp), ("ln_parts", I), ("ln_eps", Fl), ("stats_out", vp), ("tiles", I)]
 
 
 class DecodeGemmArgs(ctypes.Structure):
@@ -406,12 +406,13 @@ def dtype_code(t: torch.Tensor) -> int:
 def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ldb=None, ldc=None, bias=None,
          act=ACT_NONE, residual=None, ldr=None, aux=None, ld_aux=None, aux_scale=1.0, alpha=1.0, drop_p=0.0,
          seed=None, site=0, accumulate=False, rowsum=None, workspace=None, ln_stats=None, ln_colsum=None, ln_eps=0.0,
-         stats_out=None):
+         stats_out=None, tiles=0):
     """C = epi(alpha * A(m,k) B(k,n)); see include/mit_hip.h. Output dtype = C.dtype (f32 or operand dtype).
     rowsum: optional f32 [M] <- sum_k A(m,k) (fused bias gradient); workspace: split-K scratch, zero-filled
     once before first use (gemm_workspace(M, N, K)), one per stream. ln_stats / ln_colsum / ln_eps: the
     LayerNorm of A's rows folded in (B, bias already folded: encoder.fold_layernorm); stats_out: f32
-    [M, N / 64, 2] <- per-64-column (mean, M2) of the output rows."""
+    [M, N / 64, 2] <- per-64-column (mean, M2) of the output rows. tiles: 0 per shape, 256 / 128 the tile
+    kernel to use where it applies (256: another stream runs beside this launch)."""
     dt = dtype_code(A)
     if B.dtype != A.dtype:
         raise NativeError("gemm: A and B dtypes differ")
@@ -428,7 +429,7 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
                  ptr(residual), ldr if ldr is not None else ldc, ptr(aux), ld_aux if ld_aux is not None else ldc,
                  aux_scale, drop_p, ptr(seed), site, out_f32, 1 if accumulate else 0, ptr(rowsum), ptr(workspace),
                  0 if workspace is None else workspace.numel() * workspace.element_size(), ptr(ln_stats),
-                 ptr(ln_colsum), K // 64 if ln_stats is not None else 0, ln_eps, ptr(stats_out))
+                 ptr(ln_colsum), K // 64 if ln_stats is not None else 0, ln_eps, ptr(stats_out), tiles)
     probe = _gemm_probe
     if probe is not None:
         # algorithmic bytes: operands once, output once (+ read-back of C / residual / aux when used)
@@ -517,12 +518,13 @@ def gemm_workspace(M, N, K, device=None):
     return torch.zeros(max(gemm_workspace_bytes(M, N, K), 4096) // 4 + 4, dtype=torch.float32, device=device)
 
 
-def linear(x, w, out, *, bias=None, act=ACT_NONE, residual=None, drop_p=0.0, seed=None, site=0, workspace=None):
+def linear(x, w, out, *, bias=None, act=ACT_NONE, residual=None, drop_p=0.0, seed=None, site=0, workspace=None,
+           tiles=0):
     """out[M,N] = act(x[M,K] @ w[N,K]^T + bias) (+ residual) — nn.Linear forward."""
     M, K = x.shape[0], x.shape[-1]
     N = w.shape[0]
     gemm(x, w, out, M, N, K, lda=x.stride(0), bias=bias, act=act, residual=residual, drop_p=drop_p, seed=seed,
-         site=site, workspace=workspace)
+         site=site, workspace=workspace, tiles=tiles)
 
 
 def layernorm_fwd(x, gamma, beta, eps, y, *, r=None, drop_p=0.0, seed=None, site=0, z=None, mean=None, rstd=None,
