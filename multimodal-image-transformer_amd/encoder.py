@@ -308,6 +308,8 @@ class VisionEncoder:
         """images f32 [B,3,H,W] (already normalised) -> last_hidden_state in the compute dtype.
         rows="all": [B, N, E] ; rows="cls": only the CLS rows are finalised, returned as the
         strided view [B, E] of the [B, N, E] buffer (row stride N*E)."""
+        if self.groups_for(images.shape[0], rows) == 2:
+            return drain(self.forward_iter_groups(images, slot))
         return drain(self.forward_iter(images, rows, slot))
 
     def forward_iter(self, images: torch.Tensor, rows: str = "all", slot: int = 0, out: Optional[torch.Tensor] = None,
@@ -342,29 +344,36 @@ class VisionEncoder:
             yield
         return self._finish(B, ws, h, rows)
 
-    # f32-stream towers of at least this many rows run their prefetched forward as two image groups
-    # (CLIP-L/14@336 at B = 64, 36,928 rows: configs[2] 1879 -> 2010 pairs/s on one box). Not the ViT-B/16
+    # f32-stream towers of at least this many rows run their forward as two image groups (CLIP-L/14@336 at
+    # B = 64, 36,928 rows: configs[2] 1879 -> 2010 pairs/s; CLIP-L/14 at B = 64, 16,448 rows: configs[3]
+    # 2975 -> 3200 pairs/s, one box each, profiles/r05_clip_groups_ab.txt). Not the ViT-B/16
     # bench path (12,608 rows, folded bf16 stream): its partial rounds already hold the decoder's kernels,
     # and two groups were 1-2 % slower there (13.0-13.2 k vs 13.3 k pairs/s, profiles/r05_decoder_experiments.txt)
-    GROUP_ROWS = 32768
+    GROUP_ROWS = 16384
 
     def groups_for(self, B: int, rows: str = "all") -> int:
         """2 when forward_iter_groups applies (CLIP-L/14@336 at B = 64: 36,928 rows), else 1."""
         return 2 if (self.res32 and rows == "all" and B % 2 == 0 and B * self.N >= self.GROUP_ROWS) else 1
 
-    def forward_iter_groups(self, images: torch.Tensor, slot: int, stream2: "torch.cuda.Stream", events):
+    def forward_iter_groups(self, images: torch.Tensor, slot: int = 0):
         """forward_iter(images, "all", slot) as two image groups of B / 2, one on the current stream and
-        one on stream2, issued chunk by chunk in lockstep. Every 256-tile GEMM grid ends in a partial
+        one on the encoder's second stream, issued chunk by chunk in lockstep (forward() and the model's
+        prefetch take this path whenever groups_for says 2, so a batch's rows never depend on which ran). Every 256-tile GEMM grid ends in a partial
         round (CLIP-L/14@336, B = 64: fc2 580 tiles = 2.27 rounds of the 256 CUs, fc1 2320 = 9.06): the
         other group's kernels run in it. Each image goes through the same kernels either way (every op
-        is row- or image-wise); the result is one [B*N, E] buffer. events: a native.HipEvents pool (plan-
-        captured edges); the current stream waits for stream2 before the result is returned."""
+        is row- or image-wise); the result is one [B*N, E] buffer. The cross-stream edges are
+        native.HipEvents (captured by launch plans); the current stream waits for the second one before the
+        result is returned."""
         B = images.shape[0]
         Bg, N, E = B // 2, self.N, self.E
         key = ("groups_out", B, slot)
         if key not in self._ws:
             self._ws[key] = torch.empty(B * N, E, dtype=self.dtype, device=self.device)
         gout = self._ws[key]
+        if getattr(self, "_stream2", None) is None:
+            self._stream2 = torch.cuda.Stream(device=self.device)
+            self._gevents = native.HipEvents(8)
+        stream2, events = self._stream2, self._gevents
         s0, s1 = native.stream_ptr(), stream2.cuda_stream
         events.wait_stream(s1, s0)  # group 1 starts behind everything issued on the current stream
         # 256 tiles for every GEMM (per shape, the half-batch o-proj / fc2 would take the 128 kernel, whose

@@ -115,7 +115,6 @@ class ImageToTextModel:
         self.seed_t = torch.tensor([seed * 1000003], dtype=torch.int64, device=self.device)
         self._mem: Dict[tuple, torch.Tensor] = {}
         self._enc_stream = None
-        self._enc_stream2 = None         # the second image group's stream (encoder.forward_iter_groups)
         self._enc_slot = 0
         self._prefetched = None
         self._slot_free = None           # native.HipEvents(2): end of the backward of the step that read slot i
@@ -205,11 +204,8 @@ class ImageToTextModel:
         if self.memory_mode == "cls":
             enc = yield from self.encoder.forward_iter(images, rows="cls", slot=slot)
             return enc, N * E, 1
-        if self.encoder.groups_for(B) == 2:  # CLIP-L/14@336 at B = 64: two image groups on two streams
-            if self._enc_stream2 is None:
-                self._enc_stream2 = torch.cuda.Stream(device=self.device)
-                self._group_events = native.HipEvents(8)
-            enc = yield from self.encoder.forward_iter_groups(images, slot, self._enc_stream2, self._group_events)
+        if self.encoder.groups_for(B) == 2:  # CLIP-L towers at B = 64: two image groups on two streams
+            enc = yield from self.encoder.forward_iter_groups(images, slot)
         else:
             enc = yield from self.encoder.forward_iter(images, rows="all", slot=slot)
         return enc.reshape(B * N, E), E, N

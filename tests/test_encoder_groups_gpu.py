@@ -1,6 +1,6 @@
-"""The f32-stream encoder forward as two image groups on two streams (encoder.forward_iter_groups, the
-prefetched CLIP-L/14@336 forward of configs[2]) against the one-stream forward: bit-identical rows (every
-op is row- or image-wise, and both run the 256-tile GEMM kernel)."""
+"""The f32-stream encoder forward as two image groups on two streams (encoder.forward_iter_groups: the
+CLIP-L/14@336 and CLIP-L/14 forwards of configs[2] / configs[3]) against the one-stream forward on the same
+256-tile GEMM kernels: bit-identical rows (every op is row- or image-wise)."""
 import pytest
 import torch
 
@@ -17,14 +17,8 @@ def _lib():
     native.load_library()
 
 
-def _grouped(enc, img, slot=0):
-    s2 = torch.cuda.Stream(device=img.device)
-    ev = native.HipEvents(8)
-    return encoder.drain(enc.forward_iter_groups(img, slot, s2, ev))
-
-
-@pytest.mark.parametrize("name,B", [("openai/clip-vit-large-patch14-336", 64), ("openai/clip-vit-base-patch32", 6),
-                                    ("google/vit-base-patch16-224-in21k", 4)])
+@pytest.mark.parametrize("name,B", [("openai/clip-vit-large-patch14-336", 64), ("openai/clip-vit-large-patch14", 64),
+                                    ("openai/clip-vit-base-patch32", 6), ("google/vit-base-patch16-224-in21k", 4)])
 def test_groups_equal_one_stream(name, B):
     dev = torch.device("cuda")
     enc = encoder.build_encoder(name, dev, torch.bfloat16, seed=3)
@@ -32,17 +26,18 @@ def test_groups_equal_one_stream(name, B):
     assert enc.res32
     small = B * enc.N < enc.GROUP_ROWS
     if small:
-        # force the grouped path, and the 256-tile kernel for the one-stream forward too (per shape its
-        # small GEMMs take the 128 kernel: the same values up to the fp32 summation order)
+        # force the grouped path, and the 256-tile kernel for every GEMM (below 256 rows a half-batch GEMM
+        # takes the 128 kernel: the same values up to the fp32 summation order)
         enc.GROUP_ROWS = B * enc.N
         native.gemm_set_variant(2)
     assert enc.groups_for(B) == 2
     try:
         g = torch.Generator().manual_seed(B)
         img = torch.randn(B, 3, enc.image, enc.image, generator=g).to(dev)
-        ref = enc.forward(img, rows="all", slot=0).clone()
+        # the one-stream forward on the groups' kernels (tiles = 256) as the reference
+        ref = encoder.drain(enc.forward_iter(img, "all", 0, tiles=256)).clone()
         for slot in (0, 1):
-            out = _grouped(enc, img, slot)
+            out = encoder.drain(enc.forward_iter_groups(img, slot)) if slot else enc.forward(img, rows="all", slot=0)
             torch.cuda.synchronize()
             assert out.shape == ref.shape
             assert torch.equal(out, ref), (out.float() - ref.float()).abs().max().item()
@@ -54,20 +49,22 @@ def test_groups_only_for_large_f32_stream():
     dev = torch.device("cuda")
     enc = encoder.build_encoder("openai/clip-vit-large-patch14-336", dev, torch.bfloat16, seed=1)
     enc.configure_for("patches")
-    assert enc.groups_for(64) == 2 and enc.groups_for(32) == 1 and enc.groups_for(63) == 1
+    assert enc.groups_for(64) == 2 and enc.groups_for(32) == 2 and enc.groups_for(28) == 1 and enc.groups_for(63) == 1
     assert enc.groups_for(64, rows="cls") == 1
 
 
-def test_clip336_bench_step_grouped_prefetch_bitwise_neutral():
-    """configs[2] as bench.py runs it (CLIP-L/14@336 + 6L d512 decoder, patches memory, batch 64): steps with
-    the grouped prefetched encoder (two streams) and without a prefetch give bit-identical losses and
-    master weights, and the same steps replayed from recorded launch plans match them."""
+@pytest.mark.parametrize("workload", ["clip336", "cfg3"])
+def test_bench_step_grouped_encoder_prefetch_bitwise_neutral(workload):
+    """configs[2] / configs[3] as bench.py runs them (CLIP-L/14@336 + 6L d512 decoder / CLIP-L/14 + 12L d768
+    decoder, patches memory, batch 64; the encoder as two image groups): steps with the prefetched encoder
+    and without a prefetch give bit-identical losses and master weights, and the same steps replayed from
+    recorded launch plans match them."""
     import argparse
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    a = argparse.Namespace(workload="clip336", memory_mode="patches", vocab=10000, dtype="bf16", batch=64, seq_len=64)
+    a = argparse.Namespace(workload=workload, memory_mode="patches", vocab=10000, dtype="bf16", batch=64, seq_len=64)
     torch.cuda.set_device(0)
     res = []
     for mode in ("none", "prefetch", "replay"):

@@ -21,15 +21,13 @@ def main():
     enc.configure_for("patches")
     B = 64
     img = torch.randn(B, 3, 336, 336, device=dev)
-    s2 = torch.cuda.Stream(device=dev)
-    ev = native.HipEvents(8)
     assert enc.groups_for(B) == 2, "expected the grouped path"
 
-    def one():
-        return enc.forward(img, rows="all", slot=0)
+    def one():  # one stream, tiles per shape
+        return encoder.drain(enc.forward_iter(img, "all", 0))
 
     def grouped():
-        return encoder.drain(enc.forward_iter_groups(img, 0, s2, ev))
+        return encoder.drain(enc.forward_iter_groups(img, 0))
 
     a = one().clone()
     b = grouped().clone()
