@@ -391,29 +391,33 @@ def bench_decode(args):
 
 def also_block(args):
     """The other single-GPU BASELINE configs in the same run (N = 1, rank 0), after the headline line's
-    measurements: configs[2] (6L d512 decoder + CLIP ViT-L/14@336, 577 patches) train-step pairs/s, and
+    measurements: configs[2] (6L d512 decoder + CLIP ViT-L/14@336, 577 patches) and one GPU's share of
+    configs[3] (12L d768 decoder + CLIP ViT-L/14, 64 of the global 512 pairs) train-step pairs/s, and
     configs[4] (batched greedy decode, B = 256, max_len 100) tokens/s with the default native launch plan
-    and with one hipGraph per token step. configs[2] runs as `bench.py --workload clip336` in a child
-    process: built and replayed inside this process (after the headline model) it read 1.5-2 % lower than
+    and with one hipGraph per token step. configs[2] / configs[3] run as `bench.py --workload clip336 /
+    cfg3` in child processes: configs[2] built and replayed inside this process (after the headline model) it read 1.5-2 % lower than
     the same command alone (1853-1872 vs 1892-1899 pairs/s on one box), with or without the CPU baseline
     before it and with the headline model's state released (profiles/r05_decoder_experiments.txt)."""
     import subprocess
     out = {}
     t_all = time.perf_counter()
     steps = max(2, args.also_steps)
-    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "clip336", "--no-cpu-baseline", "--no-also",
-           "--no-roofline", "--steps", str(steps), "--warmup", "3", "--batch", str(args.batch),
-           "--seq-len", str(args.seq_len), "--vocab", str(args.vocab), "--dtype", args.dtype]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
-    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
-    if r.returncode != 0 or not lines:
-        raise RuntimeError(f"configs[2] child failed ({r.returncode}): {r.stderr[-2000:]}")
-    c = json.loads(lines[-1])
-    out["configs[2]"] = {"metric": "image-caption pairs/sec (train step), 6L/d512 decoder + CLIP ViT-L/14@336",
-                         "value": c["value"], "unit": "pairs/s", "steps": c["steps"], "ms_per_step": c["ms_per_step"],
-                         "batch": args.batch, "seq_len": args.seq_len, "dtype": c["dtype"],
-                         "step_mfma_frac": c["step_mfma_frac"], "launch_path": c["launch_path"],
-                         "process": "own: " + " ".join(["bench.py"] + cmd[2:])}
+    for key, workload, metric in (
+            ("configs[2]", "clip336", "image-caption pairs/sec (train step), 6L/d512 decoder + CLIP ViT-L/14@336"),
+            ("configs[3]", "cfg3", "image-caption pairs/sec (train step), one GPU's 64 of the global 512 pairs, "
+                                   "12L/d768 decoder + CLIP ViT-L/14")):
+        cmd = [sys.executable, os.path.abspath(__file__), "--workload", workload, "--no-cpu-baseline", "--no-also",
+               "--no-roofline", "--steps", str(steps), "--warmup", "3", "--batch", str(args.batch),
+               "--seq-len", str(args.seq_len), "--vocab", str(args.vocab), "--dtype", args.dtype]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not lines:
+            raise RuntimeError(f"{key} child failed ({r.returncode}): {r.stderr[-2000:]}")
+        c = json.loads(lines[-1])
+        out[key] = {"metric": metric, "value": c["value"], "unit": "pairs/s", "steps": c["steps"],
+                    "ms_per_step": c["ms_per_step"], "batch": args.batch, "seq_len": args.seq_len, "dtype": c["dtype"],
+                    "step_mfma_frac": c["step_mfma_frac"], "launch_path": c["launch_path"],
+                    "process": "own: " + " ".join(["bench.py"] + cmd[2:])}
     d = decode_throughput(args)
     g = decode_throughput(args, "graph")
     out["configs[4]"] = dict(d, metric="greedy caption tokens/sec (batched KV-cache decode, 6L/d512 decoder + ViT-B/16)",
