@@ -1229,7 +1229,11 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
       const int nqt = (int)((Lq + 15) / 16);
       const int maxw = (a.dropout || 2 * lkp * 256 <= 160 * 1024) ? 8 : 16;
       const int rounds = (nqt + maxw - 1) / maxw;
-      const int nw = (nqt + rounds - 1) / rounds;
+      // one workgroup per CU (the head's K/V fill the LDS: CLIP-L/14@336, 592 keys): all 16 waves, the
+      // tiles' rounds unbalanced (37 = 16 + 16 + 5), rather than 13 balanced ones (13 + 13 + 11) -- more
+      // waves to hide the sweep's latency: 47.2 -> 45.2 us, configs[2] 2067 -> 2078 pairs/s
+      // (profiles/r05_decoder_experiments.txt)
+      const int nw = maxw == 16 ? std::min(nqt, maxw) : (nqt + rounds - 1) / rounds;
       const int lds = lkp * 256;
       static bool attr = false;
       if (!attr) {
