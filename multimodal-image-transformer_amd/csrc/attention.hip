@@ -1228,12 +1228,11 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
       const int lkp = (int)((Lk + pad - 1) / pad * pad);
       const int nqt = (int)((Lq + 15) / 16);
       const int maxw = (a.dropout || 2 * lkp * 256 <= 160 * 1024) ? 8 : 16;
-      const int rounds = (nqt + maxw - 1) / maxw;
-      // one workgroup per CU (the head's K/V fill the LDS: CLIP-L/14@336, 592 keys): all 16 waves, the
-      // tiles' rounds unbalanced (37 = 16 + 16 + 5), rather than 13 balanced ones (13 + 13 + 11) -- more
-      // waves to hide the sweep's latency: 47.2 -> 45.2 us, configs[2] 2067 -> 2078 pairs/s
-      // (profiles/r05_decoder_experiments.txt)
-      const int nw = maxw == 16 ? std::min(nqt, maxw) : (nqt + rounds - 1) / rounds;
+      // every wave the occupancy allows, the query tiles' rounds unbalanced (CLIP-L/14@336: 37 = 16 + 16 + 5
+      // in one workgroup per CU; ViT-B/16: 13 = 8 + 5 in two) rather than fewer balanced waves (13 + 13 + 11,
+      // 7 + 6): more waves to hide the sweep's latency, 47.2 -> 45.2 / 26.7 -> 26.5 us, configs[2]
+      // 2067 -> 2078 pairs/s (profiles/r05_decoder_experiments.txt)
+      const int nw = std::min(nqt, maxw);
       const int lds = lkp * 256;
       static bool attr = false;
       if (!attr) {
