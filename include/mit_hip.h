@@ -240,6 +240,12 @@ typedef struct {
 int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, long Dh, const mit_attn_args* a,
                       const mit_attn_grads* g, void* stream);
 
+/* Test knob: with dropout, the head-resident / 64-query MFMA attention kernels form the mask's element
+ * index (b*H + h)*Lq*Lk + i*Lk + j in 32 bits, so calls with B*H*Lq*Lk >= limit (default 2^32) run the
+ * 64-bit-index kernels (forward attn_fwd_simple, backward attn_bwd_dq/dkv_mfma). A smaller limit sends
+ * small calls down that path (tests/test_kernels_gpu.py); limit <= 0 restores 2^32. Process-wide. */
+int mit_attention_set_index_limit(double limit);
+
 /* ---------------------------------------------------------------------------------------------
  * Encoder input assembly.
  * im2col of the patch Conv2d (tf/models/vit/modeling_vit.py:60,69; clip 148-154):

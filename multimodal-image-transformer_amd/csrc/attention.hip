@@ -1196,6 +1196,13 @@ AttnK make_k(const mit_attn_args* x) {
 }  // namespace
 
 
+// dropout calls with B*H*Lq*Lk at or past this run the 64-bit mask-index kernels (mit_attention_set_index_limit)
+static double g_idx32_limit = 4294967296.0;
+extern "C" int mit_attention_set_index_limit(double limit) {
+  g_idx32_limit = limit > 0 ? limit : 4294967296.0;
+  return MIT_OK;
+}
+
 extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, long Dh, const mit_attn_args* x,
                                  void* stream) {
   MIT_CHECK_ARG(x && x->q && x->k && x->v && x->o, "mit_attention_fwd: null pointer");
@@ -1216,7 +1223,7 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
     const long kb = 2 * ((Lk - 1) * x->k_row + D), vb = 2 * ((Lk - 1) * x->v_row + D);
     MIT_CHECK_ARG(kb < (1L << 31) && vb < (1L << 31), "mit_attention_fwd: K/V span >= 2 GiB");
     if (!a.causal && !a.tok && Lk <= HK_MAX && H <= 65535 && B <= 65535 &&
-        (!a.dropout || (double)B * (double)H * (double)Lq * (double)Lk < 4294967296.0)) {
+        (!a.dropout || (double)B * (double)H * (double)Lq * (double)Lk < g_idx32_limit)) {
       // head-resident K/V: one workgroup per (b, h), NW waves balanced over the 16-query tiles.
       // K/V rows are staged to a multiple of 16 (the key tail of < 64 runs 16-key tiles: a ViT-B/16
       // head of 197 keys sweeps 208 instead of 256; 28.5 -> 27.7 us, tools/attn_bench.py). <= 8 waves
@@ -1247,7 +1254,7 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
         hipLaunchKernelGGL(attn_fwd_head<true>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
       else
         hipLaunchKernelGGL(attn_fwd_head<false>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
-    } else if (!a.dropout || (double)B * (double)H * (double)Lq * (double)Lk < 4294967296.0) {
+    } else if (!a.dropout || (double)B * (double)H * (double)Lq * (double)Lk < g_idx32_limit) {
       hipLaunchKernelGGL(attn_fwd_mfma, grid, dim3(256), 0, s, H, Lq, Lk, a, (int)kb, (int)vb);
     } else {  // dropout indices past 2^32 (the MFMA kernels form them in 32 bits)
       hipLaunchKernelGGL((attn_fwd_simple<bf16, 64>), grid, dim3(64), 0, s, H, Lq, Lk, a);
@@ -1297,7 +1304,7 @@ extern "C" int mit_attention_bwd(int dtype, long B, long H, long Lq, long Lk, lo
     nb.dO = (int)db;
     // (the head kernel forms its dropout indices in 32 bits: B * H * Lq * Lk < 2^32)
     if (Lq <= 64 && Lk <= HB_MAXK && H <= 65535 && B <= 65535 && x->o_row % 8 == 0 &&
-        (double)B * (double)H * (double)Lq * (double)Lk < 4294967296.0) {
+        (double)B * (double)H * (double)Lq * (double)Lk < g_idx32_limit) {
       const int lkp = (int)((Lk + 31) / 32 * 32);
       const int lds = 2 * lkp * 128 + 2 * 64 * 128 + 2 * 64 * 4;
       static bool attr = false;

@@ -24,7 +24,7 @@ int mit_set_error(const char* fmt, ...) {
 }
 
 extern "C" const char* mit_last_error(void) { return g_err; }
-extern "C" int mit_abi_version(void) { return 5; }
+extern "C" int mit_abi_version(void) { return 6; }
 
 // ---------------------------------------------------------------------------------------------
 // launch plans

@@ -142,21 +142,24 @@ __device__ __forceinline__ float quick_gelu(float x) {
   quick_gelu_n<1>(&x);
   return x;
 }
-// GELU (erf form) for bf16 epilogues with ONE transcendental and no select: x Phi(x) = max(x, 0) - |x| h,
-// h = Phi(-|x|) = 2^q(a), a = min(|x|, 6), q a degree-7 fit of log2 Phi(-a) on [0, 6] (tools/gelu_fit.py):
+// GELU (erf form) for bf16 epilogues with ONE transcendental and no select: x Phi(x) = max(x, 0) - a h,
+// a = min(|x|, 6), h = Phi(-a) = 2^q(a), q a degree-7 fit of log2 Phi(-a) on [0, 6] (tools/gelu_fit.py):
 // relative error <= 6.6e-6 for |x| <= 6 (1/300 of a bf16 half-ulp; the negative tail keeps its relative
-// accuracy, no 1 - 1), |error| <= 1.2e-8 below -6. 10 VALU + one v_exp_f32, against the A&S 7.1.26
-// form's rcp + exp + compare / select; fp32 parity mode keeps gelu_erf.
+// accuracy, no 1 - 1). Past |x| = 6 the correction term is the constant 6 Phi(-6) = 5.9e-9, so the error
+// stays <= 5.9e-9 absolute for every x (a = |x| there would grow it with |x|, and turn x = +inf into
+// inf - inf); x = +-inf gives +inf / -5.9e-9. a is the NaN-propagating minimum (v_minimum3_f32, one op like
+// v_min_f32), so a NaN input stays NaN. 10 VALU + one v_exp_f32, against the A&S 7.1.26 form's rcp + exp +
+// compare / select; fp32 parity mode keeps gelu_erf.
 #define MIT_GELU_Q(F) F(-1.834813247e-06f), F(6.159832992e-05f), F(-9.305251297e-04f), F(8.507891558e-03f), \
                       F(-5.396007001e-02f), F(-4.584643841e-01f), F(-1.151251078e+00f), F(-9.999952912e-01f)
 #define MIT_GELU_S(c) c
 __device__ __forceinline__ float gelu_fast(float x) {
   constexpr float q[8] = {MIT_GELU_Q(MIT_GELU_S)};
-  const float a = fminf(fabsf(x), 6.0f);
+  const float a = __builtin_elementwise_minimum(fabsf(x), 6.0f);
   float p = fmaf(q[0], a, q[1]);
 #pragma unroll
   for (int k = 2; k < 8; ++k) p = fmaf(p, a, q[k]);
-  return fmaf(-fabsf(x), __builtin_amdgcn_exp2f(p), fmaxf(x, 0.0f));
+  return fmaf(-a, __builtin_amdgcn_exp2f(p), fmaxf(x, 0.0f));
 }
 
 // gelu_fast on two values: the polynomial in packed FP32 (v_pk_fma_f32, two values per instruction);
@@ -164,12 +167,12 @@ __device__ __forceinline__ float gelu_fast(float x) {
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
   constexpr float q[8] = {MIT_GELU_Q(MIT_GELU_S)};
-  const f32x2 a = {fminf(fabsf(x[0]), 6.0f), fminf(fabsf(x[1]), 6.0f)};
+  const f32x2 a = {__builtin_elementwise_minimum(fabsf(x[0]), 6.0f), __builtin_elementwise_minimum(fabsf(x[1]), 6.0f)};
   f32x2 p = __builtin_elementwise_fma(f32x2{q[0], q[0]}, a, f32x2{q[1], q[1]});
 #pragma unroll
   for (int k = 2; k < 8; ++k) p = __builtin_elementwise_fma(p, a, f32x2{q[k], q[k]});
-  return f32x2{fmaf(-fabsf(x[0]), __builtin_amdgcn_exp2f(p[0]), fmaxf(x[0], 0.0f)),
-               fmaf(-fabsf(x[1]), __builtin_amdgcn_exp2f(p[1]), fmaxf(x[1], 0.0f))};
+  return f32x2{fmaf(-a[0], __builtin_amdgcn_exp2f(p[0]), fmaxf(x[0], 0.0f)),
+               fmaf(-a[1], __builtin_amdgcn_exp2f(p[1]), fmaxf(x[1], 0.0f))};
 }
 #undef MIT_GELU_S
 #undef MIT_GELU_Q

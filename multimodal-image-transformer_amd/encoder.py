@@ -292,8 +292,7 @@ class VisionEncoder:
                 qkv=torch.empty(R, 3 * E, dtype=dt, device=dev),
                 o=torch.empty(R, E, dtype=dt, device=dev),
                 m=torch.empty(R, self.mlp, dtype=dt, device=dev),
-                out=torch.empty(R, E, dtype=dt, device=dev),
-            )
+            )  # "out" (the ViT final LayerNorm / f32-stream result) is allocated on first use: _out
             if self.fold_ln:  # per-64-column (mean, M2) of the residual stream's rows
                 self._ws[key]["st"] = torch.empty(R, E // 64, 2, dtype=torch.float32, device=dev)
             if self.res32:  # f32 residual stream, the bf16 sublayer output (delta) and CLIP's f32 embeddings
@@ -303,6 +302,14 @@ class VisionEncoder:
                 ws["pt32"] = torch.empty(R, E, dtype=torch.float32, device=dev)
                 del ws["pt"], ws["h"]
         return self._ws[key]
+
+    def _out(self, ws):
+        """The arena's result rows [B*N, E], allocated when a forward first writes them there (the grouped
+        forward's per-group arenas write into the shared groups_out buffer instead and never allocate it:
+        ~150 MB across its 2 slots x 2 groups at CLIP-L/14@336, B = 64)."""
+        if "out" not in ws:
+            ws["out"] = torch.empty(ws["qkv"].shape[0], self.E, dtype=self.dtype, device=self.device)
+        return ws["out"]
 
     def forward(self, images: torch.Tensor, rows: str = "all", slot: int = 0) -> torch.Tensor:
         """images f32 [B,3,H,W] (already normalised) -> last_hidden_state in the compute dtype.
@@ -464,7 +471,7 @@ class VisionEncoder:
             pend = d
             yield
         N = self.N
-        out = ws["out"] if out is None else out
+        out = self._out(ws) if out is None else out
         if self.kind == "vit":
             if rows == "cls":
                 native.layernorm_fwd_x32(h32, w["final_ln.w"], w["final_ln.b"], self.eps, out, r=pend, rows=B,
@@ -481,7 +488,7 @@ class VisionEncoder:
     def _finish(self, B, ws, h, rows):
         w, E, N = self.w, self.E, self.N
         if self.kind == "vit":
-            out = ws["out"]
+            out = self._out(ws)
             if rows == "cls":
                 native.layernorm_fwd(h, w["final_ln.w"], w["final_ln.b"], self.eps, out, rows=B, cols=E, ldx=N * E,
                                      ldy=N * E)

@@ -189,6 +189,7 @@ class ImageToTextModel:
     # --- memory (encoder -> projection) ----------------------------------------------------------
     def _encoder_rows(self, images: torch.Tensor, slot: int = 0):
         """Frozen encoder -> (enc_rows, enc_ld, S): the rows that feed the projection."""
+        self.encoder.configure_for(self.memory_mode)  # memory_mode may have changed since __init__ (cheap)
         B = images.shape[0]
         N, E = self.encoder.N, self.encoder.E
         if self.memory_mode == "cls":
@@ -199,6 +200,7 @@ class ImageToTextModel:
 
     def _encoder_rows_iter(self, images: torch.Tensor, slot: int = 0):
         """_encoder_rows as a generator of launch chunks (VisionEncoder.forward_iter)."""
+        self.encoder.configure_for(self.memory_mode)
         B = images.shape[0]
         N, E = self.encoder.N, self.encoder.E
         if self.memory_mode == "cls":

@@ -13,12 +13,21 @@ import ctypes
 import os
 from typing import Optional
 
-import torch
+# Hardware queues per process (read once, when HIP initialises: set before the first HIP call). A train step
+# runs on up to five streams -- main, weight-gradient side stream, encoder prefetch, the CLIP towers' second
+# encoder stream, and under data parallelism RCCL's stream (ProcessGroupNCCL) -- and HIP's default of 4 queues
+# makes two of them share one: a stream-wait on the shared queue then stalls the other stream's kernels too.
+# Measured on one MI355X (bench.py --dp, one RCCL rank, native replay): 4 queues 10.0 k pairs/s, 8 queues
+# 13.6 k, 16 queues 13.6 k; the plain one-process step 13.7 k with 4 or 8 (profiles/r06_dp1_nccl_run.json).
+# The driver's multi-GPU bench runs exactly the RCCL path. An explicit setting in the environment wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
+import torch  # noqa: E402
 from torch.utils._python_dispatch import TorchDispatchMode
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MIT_HIP_LIB", os.path.join(_HERE, "lib", "libmit_hip.so"))
-ABI_VERSION = 5  # mit_abi_version() of the library this binding matches (include/mit_hip.h)
+ABI_VERSION = 6  # mit_abi_version() of the library this binding matches (include/mit_hip.h)
 
 F32, BF16 = 0, 1
 K_CONTIG, MN_CONTIG = 0, 1
@@ -91,6 +100,7 @@ SIGNATURES = {
     "mit_layernorm_param_grads": (I, [L, L, vp, vp, vp, vp]),
     "mit_attention_fwd": (I, [I, L, L, L, L, L, ctypes.POINTER(AttnArgs), vp]),
     "mit_attention_bwd": (I, [I, L, L, L, L, L, ctypes.POINTER(AttnArgs), ctypes.POINTER(AttnGrads), vp]),
+    "mit_attention_set_index_limit": (I, [ctypes.c_double]),
     "mit_im2col": (I, [I, L, L, L, L, L, vp, vp, L, vp]),
     "mit_vit_assemble": (I, [I, L, L, L, vp, vp, vp, vp, vp]),
     "mit_embed_fwd": (I, [I, L, L, L, vp, vp, Fl, vp, Fl, vp, U32, vp, vp]),
@@ -494,6 +504,12 @@ def set_gemm_probe(probe):
     every GEMM launch (bench.py records HIP events there to time the GEMM kernels in place)."""
     global _gemm_probe
     _gemm_probe = probe
+
+
+def attention_set_index_limit(limit: float = 0.0):
+    """Test knob (mit_attention_set_index_limit): dropout attentions with B*H*Lq*Lk >= limit run the 64-bit
+    mask-index kernels; 0 restores the default 2^32."""
+    _check(lib().mit_attention_set_index_limit(float(limit)), "mit_attention_set_index_limit")
 
 
 def gemm_set_variant(v):

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(native.LIB_PATH)
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, f"missing exports: {missing}"
-    assert lib.mit_abi_version() == 5
+    assert lib.mit_abi_version() == 6
 
 
 def test_python_binding_covers_header():

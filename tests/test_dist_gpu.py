@@ -87,6 +87,12 @@ def test_dp2_train_step_on_hip_path_matches_reference(world, backend):
         assert p.exitcode == 0
     assert abs(loss - T["loss"].item()) < 1e-4
     assert abs(total - T["grad_total_norm_preclip"].item()) < 1e-3 * total
+    _check_against_reference(meta, T, grad, coef, {k: torch.from_numpy(v) for k, v in deltas.items()})
+
+
+def _check_against_reference(meta, T, grad, coef, deltas):
+    """The flat gradient (pre-clip, times the clip coefficient) and the AdamW update of every trainable
+    tensor against the reference's step (dp2_tiny's grad1 / delta1 statistics)."""
     from decoder import decoder_entries, flat_to_reference
     from params import FlatParams
     dec, enc = FX.dec_desc(meta), FX.enc_desc(meta)
@@ -94,7 +100,6 @@ def test_dp2_train_step_on_hip_path_matches_reference(world, backend):
     store = FlatParams(decoder_entries(dec["vocab"], dec["d"], dec["layers"], dec["ff"],
                                        E if E != dec["d"] else None), torch.device("cpu"), torch.float32)
     store.grad.copy_(torch.from_numpy(grad))
-    deltas = {k: torch.from_numpy(v) for k, v in deltas.items()}
 
     class GV:
         vocab = dec["vocab"]
@@ -183,3 +188,118 @@ def test_bench_spawns_its_own_ranks():
     assert len(lines) == 1, r.stdout[-2000:]
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 16 and rec["value"] > 0
+
+
+
+def _replay_worker(port, q):
+    """ONE rank over RCCL (ProcessGroupNCCL, world size 1): the launch path bench.py --gpus N takes on the
+    driver's 8-GPU node -- DataParallel(overlap=True), train_step(next_images=...) with the encoder prefetch,
+    steps recorded by native.record (the bucket all-reduces and the count all-reduce as recorded host steps
+    between native plans) and replayed by mit_plan_run. Two models from the same weights: "eager" runs 5
+    eager steps; "replay" runs step 1 eager (arenas, optimizer state and split-K scratch are set up by a real
+    step first, as bench.py's warm-up does), records steps 2-3 (run for real while recording) and replays
+    the two programs as steps 4-5. Reports each step's loss, the final master / AdamW moments / dropout seed
+    of both, and the eager run's step-1 loss, gradient, clip norm and update (the reference comparison).
+    fp32 without dropout (the reference's step) and bf16 with dropout 0.1 (the bench's arithmetic: the
+    replayed steps must advance the dropout seed and the AdamW step exactly as eager steps do)."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(here, "..", "multimodal-image-transformer_amd"), os.path.join(here, "golden")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import fixtures as FX
+        import native
+        import optim
+        from dist import DataParallel
+        from model_util import build_model
+        import procedural as P
+        meta, T = FX.load("dp2_tiny")
+        imgs = P.make_images(meta["B"], meta["image_size"], meta["seed"] + 1).cuda()
+        cap = P.make_captions(meta["B"], meta["cap_len"], meta["dec"]["vocab"], meta["seed"] + 2, meta["lengths"])
+        di, tg = cap[:, :-1].contiguous().cuda(), cap[:, 1:].contiguous().cuda()
+        names = FX.trainable_names(meta)
+        out = {"backend": dist.get_backend()}
+        for tag, dtype, p in (("f32", torch.float32, 0.0), ("bf16", torch.bfloat16, 0.1)):
+            runs = {}
+            for mode in ("eager", "replay"):
+                m, _ = build_model(meta, dtype, dropout=p)
+                m.train()
+                dp = DataParallel(m, overlap=True)
+                opt = optim.AdamW(m.store, lr=meta["lr"], betas=tuple(meta["betas"]), eps=meta["eps"],
+                                  weight_decay=meta["weight_decay"])
+                held = {}
+
+                def step():
+                    held["loss"] = m.train_step(imgs, di, tg, dist=dp, next_images=imgs)
+                    opt.step(meta["clip"])
+
+                # step 1, eager in both runs; the eager run keeps its gradient and update for the reference
+                before = {k: v.clone() for k, v in m.state_dict().items() if k in names}
+                held["loss"] = m.train_step(imgs, di, tg, dist=dp, next_images=imgs)
+                torch.cuda.synchronize()
+                grad1 = m.store.grad.clone().cpu().numpy()
+                opt.step(meta["clip"])
+                after = m.state_dict()
+                first = dict(loss=held["loss"].item(), grad=grad1, norm=opt.norm_t.cpu().tolist(),
+                             delta={k: (after[k] - before[k]).cpu().numpy() for k in names})
+                losses = [first["loss"]]
+                if mode == "eager":
+                    for _ in range(4):
+                        step()
+                        losses.append(held["loss"].item())
+                else:
+                    progs = []
+                    for _ in range(2):
+                        progs.append(native.record(step))
+                        losses.append(held["loss"].item())
+                    for i in range(2):
+                        opt._sync_lr()
+                        progs[i].run()
+                        losses.append(held["loss"].item())
+                    out.setdefault("launches", progs[0].launches())
+                torch.cuda.synchronize()
+                st = m.store
+                runs[mode] = dict(losses=losses, master=st.master.cpu().numpy(), exp_avg=st.exp_avg.cpu().numpy(),
+                                  exp_avg_sq=st.exp_avg_sq.cpu().numpy(), seed=m.seed_t.cpu().numpy(),
+                                  first=first if mode == "eager" else None)
+                del m, dp, opt, held
+                torch.cuda.synchronize()
+            out[tag] = runs
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_one_rank_native_replay_matches_eager_and_reference():
+    """The driver's N-GPU launch path (native record / replay with the DP collectives as host steps and the
+    encoder prefetch), run under RCCL at world size 1 on this one-GPU box: replayed steps bit-identical to
+    eager ones (losses, master weights, AdamW moments, dropout seed), step 1 equal to the reference's
+    single-process step on dp2_tiny (train.py:62-123 at B = 8)."""
+    import numpy as np
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    meta, T = FX.load("dp2_tiny")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    pr = ctx.Process(target=_replay_worker, args=(port, q))
+    pr.start()
+    out = q.get(timeout=300)
+    pr.join(timeout=60)
+    assert pr.exitcode == 0
+    assert out["backend"] == "nccl" and out["launches"] > 0
+    for tag in ("f32", "bf16"):
+        e, r = out[tag]["eager"], out[tag]["replay"]
+        assert e["losses"] == r["losses"], (tag, e["losses"], r["losses"])
+        assert len(set(e["losses"])) > 1, (tag, e["losses"])  # the steps did update the weights
+        for k in ("master", "exp_avg", "exp_avg_sq", "seed"):
+            assert np.array_equal(e[k], r[k]), (tag, k)
+    f = out["f32"]["eager"]["first"]
+    assert abs(f["loss"] - T["loss"].item()) < 1e-4
+    total, coef = f["norm"]
+    assert abs(total - T["grad_total_norm_preclip"].item()) < 1e-3 * total
+    _check_against_reference(meta, T, f["grad"], coef, {k: torch.from_numpy(v) for k, v in f["delta"].items()})

@@ -160,6 +160,46 @@ def test_gemm_gelu_epilogue_accuracy():
         assert err < 2e-5 * ref.abs().max().item(), (v, err)
 
 
+def test_gemm_gelu_epilogue_extremes():
+    """The one-exp GELU past its fit range (common.h gelu_fast / gelu_fast2): +inf -> +inf (not inf - inf),
+    -inf and large negative -> 0 within 5.9e-9 (the correction term is capped at 6 Phi(-6), it does not grow
+    with |x|), large positive -> x, NaN -> NaN. Injected through the bias columns, f32 and bf16 outputs, on
+    the 128 kernel's vector epilogue (variant 1) and the 256 kernel's staged one (variant 2)."""
+    M, Nn, K = 512, 776, 256
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(M, K, generator=g).to(dev(), torch.bfloat16)
+    w = (torch.randn(Nn, K, generator=g) / 8).to(dev(), torch.bfloat16)
+    special = [float("inf"), float("-inf"), float("nan"), -1000.0, 1000.0, -1e30, 1e30]
+    moderate = [-7.0, 7.0, -6.0, 6.0, -6.5, 6.5]  # checked against the reference with the other columns
+    bias = torch.randn(Nn, generator=g) * 0.1
+    cols = list(range(3, 3 + 8 * len(special), 8))
+    for c, b in zip(cols, special):
+        bias[c] = b
+    for i, b in enumerate(moderate):
+        bias[500 + 8 * i] = b
+    bias = bias.to(dev())
+    rest = [c for c in range(Nn) if c not in cols]
+    ref = F.gelu(x.double() @ w.double().t() + bias.double()).cpu()[:, rest]
+    for v in (1, 2):
+        N.gemm_set_variant(v)
+        for odt in (torch.float32, torch.bfloat16):
+            out = torch.empty(M, Nn, device=dev(), dtype=odt)
+            N.gemm(x, w, out, M, Nn, K, bias=bias, act=N.ACT_GELU)
+            o = out.double().cpu()
+            for c, b in zip(cols, special):
+                col = o[:, c]
+                if b != b:
+                    assert torch.isnan(col).all(), (v, odt, b)
+                elif b == float("inf") or b == 1e30:
+                    assert (col == torch.tensor(b).to(odt).double()).all(), (v, odt, b)
+                elif b > 0:
+                    assert ((col - b).abs() <= 16).all(), (v, odt, b)
+                else:  # -inf, -1e30, -1000: GELU -> 0; the capped correction leaves at most 5.9e-9
+                    assert (col.abs() <= 6e-9).all() and not torch.isnan(col).any(), (v, odt, b, col.abs().max())
+            tol = 1e-2 if odt == torch.bfloat16 else 2e-5
+            assert (o[:, rest] - ref).abs().max().item() < tol * ref.abs().max().item(), (v, odt)
+
+
 @pytest.mark.parametrize("M,Nn,K", [(4032, 512, 512), (4032, 512, 2048), (256, 10000, 512), (250, 520, 200),
                                     (1000, 136, 1096), (64, 64, 64), (70, 2048, 72)])
 def test_register_streaming_kernel(M, Nn, K):

@@ -549,3 +549,17 @@ def test_embed_plan_matches_stable_sort(n):
         runs[k] = j - k
         k = j
     assert p[n:].tolist() == runs
+
+
+@pytest.mark.parametrize("kind", ["self_drop", "cross_drop", "cross_drop40", "cross_drop17"])
+def test_attention_dropout_64bit_index_path(kind):
+    """Dropout attentions whose mask index B*H*Lq*Lk reaches 2^32 run the 64-bit-index kernels (forward
+    attn_fwd_simple, backward attn_bwd_dq/dkv_mfma): mit_attention_set_index_limit(1) sends these small
+    calls down that path. The forward and the backward must rebuild the SAME mask (mix_u32's 64-bit index:
+    high half rotated in, zero here) -- checked through outputs, lse and all three gradients against torch
+    with the mask from mit_dropout_mask."""
+    N.attention_set_index_limit(1.0)
+    try:
+        test_attention_fwd_bwd(torch.bfloat16, 64, kind)
+    finally:
+        N.attention_set_index_limit(0.0)
