@@ -123,8 +123,18 @@ __device__ __forceinline__ float quick_gelu_core(float x) {
 // the division when any |x| > 51 or is not finite (d near or past the float range). Bitwise identical to
 // quick_gelu_ieee over all 2^32 inputs (tools/qgelu_exhaustive.hip); per-value branches cost more than the
 // expansion they save (CLIP fc1 374 vs 343 us)
+// MIT_QGELU_RCP (variant builds only, tools/build_variants.sh): the plain x * rcp(d) form, ~1 ulp off the
+// division -- the round-5 variant whose effect on cfg3's gradient metric tools/grad_metric_report.py measures
+#ifndef MIT_QGELU_RCP
+#define MIT_QGELU_RCP 0
+#endif
 template <int N>
 __device__ __forceinline__ void quick_gelu_n(float* v) {
+  if constexpr (MIT_QGELU_RCP) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = v[k] * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[k]));
+    return;
+  }
   float x[N];
   bool slow = false;
 #pragma unroll

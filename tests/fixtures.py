@@ -30,6 +30,22 @@ def load(name: str):
     return meta, tensors
 
 
+@lru_cache(maxsize=None)
+def load_dense(name: str):
+    """The denser gradient pins of a fixture (tests/golden/make_grad_dense.py: 1024 elements per tensor of
+    more than 4096, a superset of the fixture's 64), as {tensor name: (index LongTensor, reference values)};
+    None for fixtures without them."""
+    path = os.path.join(GOLDEN, f"{name}.grad_dense.safetensors")
+    if not os.path.exists(path):
+        return None
+    with safe_open(path, "pt") as f:
+        meta = json.loads(f.metadata()["meta"])
+        vals = {k[len("grad1.dense."):]: f.get_tensor(k) for k in f.keys()}
+    fx_meta, _ = load(name)
+    numel = {n: int(torch.tensor(s).prod()) for n, s in fx_meta["spec"]}
+    return {n: (P.sample_index(numel[n], meta["k"], meta["seeds"][n]), v) for n, v in vals.items()}
+
+
 def enc_desc(meta) -> dict:
     """Encoder geometry from the fixture's HF config kwargs (ViTConfig()/CLIPVisionConfig() defaults)."""
     c = dict(meta["enc_cfg"])

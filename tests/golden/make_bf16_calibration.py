@@ -63,6 +63,10 @@ def main():
         total = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g) for g in grads])).item()
         coef = min(1.0, meta["clip_first"] / (total + 1e-6))
         ge = {k: rms_err("grad1", k, params[k].grad * coef, T, meta) for k in names}
+        dense = FX.load_dense(name)
+        if dense is not None:  # the same metric over the denser pins (make_grad_dense.py, 1024 per tensor)
+            from parity_metrics import dense_metrics
+            r.update(dense_metrics(names, {k: params[k].grad * coef for k in names}, T, dense))
         r.update({"step1_loss_abs_err": abs(loss.item() - T["step1.loss"].item()),
                   "grad_norm_rel_err": abs(total - T["step1.grad_total_norm_preclip"].item()) / total,
                   "grad_rms_median": sorted(ge.values())[len(ge) // 2], "grad_rms_max": max(ge.values()),

@@ -28,12 +28,66 @@ def tensor_err(prefix, name, t, T, meta):
     return rms_err / max(rn / n ** 0.5, 1e-30), abs(float(t.norm()) - rn) / max(rn, 1e-30)
 
 
+def dense_err(name, t, T, dense, trim=0.0):
+    """tensor_err's RMS ratio over the denser pins (FX.load_dense: 1024 elements) instead of the 64; for
+    tensors stored whole it is tensor_err's. trim > 0: the largest ceil(trim * pins) squared errors are left out
+    first (a trimmed RMS: the per-element errors are heavy-tailed -- a bf16 ReLU-boundary flip moves a whole
+    row of a linear1 weight gradient -- so the plain RMS of a sample is carried by a handful of elements,
+    tools/grad_metric_report.py). Returns (ratio, per-element squared-error shares sorted descending)."""
+    t = t.detach().float().cpu().flatten()
+    if f"grad1.full.{name}" in T:
+        ref = T[f"grad1.full.{name}"].flatten()
+        rms_t = float(ref.norm()) / t.numel() ** 0.5
+        e2 = (t - ref) ** 2
+    else:
+        idx, ref = dense[name]
+        rms_t = float(T[f"grad1.stats.{name}"][1]) / t.numel() ** 0.5
+        e2 = (t[idx] - ref) ** 2
+    srt = e2.sort(descending=True)[0]
+    share = srt / srt.sum().clamp_min(1e-30)
+    if trim > 0:
+        srt = srt[int(-(-trim * srt.numel() // 1)):]
+    return float(srt.mean().sqrt()) / max(rms_t, 1e-30), share
+
+
+def dense_metrics(names, grads, T, dense):
+    """Worst / median over the tensors of dense_err: plain ("_dense") and 1 %-trimmed ("_trim")."""
+    r = {}
+    for tag, trim in (("dense", 0.0), ("trim", 0.01)):
+        de = {k: dense_err(k, grads[k], T, dense, trim)[0] for k in names}
+        r.update({f"grad_rms_max_{tag}": max(de.values()), f"grad_rms_worst_{tag}": max(de, key=de.get),
+                  f"grad_rms_median_{tag}": sorted(de.values())[len(de) // 2]})
+    return r
+
+
+def step1(m, meta, imgs, di, tg):
+    """The fixture's first train step (train.py:80-100: forward, CE, backward, clip_first, AdamW) on the HIP
+    path. Returns (loss, pre-clip total norm, clip coefficient, {reference tensor name: gradient})."""
+    import optim
+    from decoder import flat_to_reference
+    m.train()
+    opt = optim.AdamW(m.store, lr=meta["lr"], betas=tuple(meta["betas"]), eps=meta["eps"],
+                      weight_decay=meta["weight_decay"])
+    l1 = m.train_step(imgs.cuda(), di.cuda(), tg.cuda()).item()
+    opt.step(meta["clip_first"])
+    total, coef = opt.norm_t.tolist()
+
+    class GV:
+        vocab = m.decoder.V
+
+        def p(self, n):
+            return m.store.g(n)
+
+    grads = flat_to_reference(GV(), m.decoder.L, m.decoder_embed_dim)
+    if m.has_projection:
+        grads["projection.weight"] = m.store.g("projection.weight")
+        grads["projection.bias"] = m.store.g("projection.bias")
+    return l1, total, coef, grads
+
 
 def case_metrics(name, dtype):
     """encoder rows, logits, argmax, loss, and one train step (train.py:80-100) of the HIP path at
     `dtype` against the reference's fp32 outputs."""
-    import optim
-    from decoder import flat_to_reference
     meta, T = FX.load(name)
     m, _ = build_model(meta, dtype)
     imgs, di, tg = FX.inputs(meta, 0)
@@ -53,31 +107,18 @@ def case_metrics(name, dtype):
          "logits_max_abs_over_scale": float((got - ref).abs().max() / ref.abs().max()),
          "argmax_agree_margin_gt_5e-2": float((logits.argmax(-1).float()[safe] == T["fwd.argmax"][safe]).float().mean()),
          "loss_abs_err": abs(loss - T["fwd.loss"].item())}
-    m.train()
-    opt = optim.AdamW(m.store, lr=meta["lr"], betas=tuple(meta["betas"]), eps=meta["eps"],
-                      weight_decay=meta["weight_decay"])
     names = FX.trainable_names(meta)
     before = {k: v.clone() for k, v in m.state_dict().items() if k in names}
-    l1 = m.train_step(imgs.cuda(), di.cuda(), tg.cuda()).item()
-    opt.step(meta["clip_first"])
-    total, coef = opt.norm_t.tolist()
-
-    class GV:
-        vocab = m.decoder.V
-
-        def p(self, n):
-            return m.store.g(n)
-
-    grads = flat_to_reference(GV(), m.decoder.L, m.decoder_embed_dim)
-    if m.has_projection:
-        grads["projection.weight"] = m.store.g("projection.weight")
-        grads["projection.bias"] = m.store.g("projection.bias")
+    l1, total, coef, grads = step1(m, meta, imgs, di, tg)
     after = m.state_dict()
     ge = {k: tensor_err("grad1", k, grads[k] * coef, T, meta) for k in names}
     gerr = {k: v[0] for k, v in ge.items()}
     gnorm = {k: v[1] for k, v in ge.items()}
     derr = {k: tensor_err("delta1", k, after[k] - before[k], T, meta)[0] for k in names
             if not k.endswith("in_proj_bias")}
+    dense = FX.load_dense(name)
+    if dense is not None:  # the same metric over 1024 pinned elements per tensor (make_grad_dense.py)
+        r.update(dense_metrics(names, {k: grads[k] * coef for k in names}, T, dense))
     r.update({"step1_loss_abs_err": abs(l1 - T["step1.loss"].item()),
               "grad_norm_rel_err": abs(total - T["step1.grad_total_norm_preclip"].item()) / total,
               "grad_rms_max": max(gerr.values()), "grad_rms_worst": max(gerr, key=gerr.get),

@@ -14,7 +14,11 @@ so no bf16 implementation meets 1e-2 absolute; DESIGN.md §6 has the table. Boun
            tensor's norm within 10 %.
   The 24-layer CLIP-L configs (cfg2, cfg3: f32 encoder residual stream) are held tighter: logits
   rel-L2 <= 8e-3, encoder <= 1.3x and worst gradient tensor <= 1.5x the reference's bf16 error
-  (measured round 3: 6.8e-3 / 7.4e-3, 1.00x / 0.98x, 1.05x / 1.22x; profiles/r03_bf16_parity.json).
+  (measured round 3: 6.8e-3 / 7.4e-3, 1.00x / 0.98x, 1.05x / 1.22x; profiles/r03_bf16_parity.json). Since
+  round 6 that worst-tensor bound is taken over 1024 pinned elements per tensor (tests/golden/
+  make_grad_dense.py) with the largest 1 % of squared errors left out: over the fixtures' 64 pins a
+  handful of elements carried each tensor's value (tools/grad_metric_report.py,
+  profiles/r06_grad_metric_report.json).
   Margin: every fixture's logits rel-L2 <= 1.15x the reference's bf16 error and >= 10 %
   under the 1e-2 bound (<= 9e-3). Each case's metrics are written to gpurun_out/parity/<case>.json
   (and printed), so the margin of the tree under test is on record after every GPU run."""
@@ -64,4 +68,7 @@ def test_bf16_within_reference_bf16_envelope(name):
     if name.startswith(("cfg2", "cfg3")):  # 24-layer CLIP-L towers, f32 encoder residual stream
         assert r["logits_rel_l2"] <= 8e-3
         assert r["enc_rel_l2"] <= 1.3 * c["enc_rel_l2"]
-        assert r["grad_rms_max"] <= 1.5 * c["grad_rms_max"]
+        # the worst tensor over the 1024 denser pins, 1 % trimmed (round 6, profiles/r06_grad_metric_report.json):
+        # on 64 pins one to four elements carry 70-93 % of a tensor's squared error, so the max over ~150
+        # tensors jumped 1.3-1.7x under a 1-ulp quick_gelu change; this form moved 0.2-0.9 % under it
+        assert r["grad_rms_max_trim"] <= 1.5 * c["grad_rms_max_trim"]
