@@ -32,6 +32,8 @@ extern "C" {
 enum { MIT_F32 = 0, MIT_BF16 = 1 };
 enum { MIT_K_CONTIG = 0, MIT_MN_CONTIG = 1 };
 enum { MIT_ACT_NONE = 0, MIT_ACT_RELU = 1, MIT_ACT_GELU = 2, MIT_ACT_QUICK_GELU = 3 };
+/* slots per row of the decode head's argmax keys (mit_decode_gemm_args.argmax_keys, mit_greedy_pick_keys) */
+#define MIT_ARGMAX_SLOTS 16
 
 const char* mit_last_error(void);
 int mit_abi_version(void);
@@ -339,8 +341,9 @@ int mit_greedy_pick(long B, long V, const float* logits, long ld, int64_t* ids, 
  * separate mit_step_inc launch folded in. */
 int mit_greedy_pick_advance(long B, long V, const float* logits, long ld, int64_t* ids, long ld_ids, int64_t* pos,
                             int64_t end_id, int64_t pad_id, int* finished, int* n_finished, int* ticket, void* stream);
-/* greedy_pick_advance from the argmax keys a mit_decode_gemm (argmax_keys) left: column
- * 0xFFFFFFFF - (u32)keys[b] is row b's pick; the keys are reset to 0 and *pos advanced (one block). */
+/* greedy_pick_advance from the argmax keys a mit_decode_gemm (argmax_keys) left (u64 [MIT_ARGMAX_SLOTS][B]):
+ * with k the largest of row b's slot keys, column 0xFFFFFFFF - (u32)k is its pick; the keys are reset to 0
+ * and *pos advanced (one block). */
 int mit_greedy_pick_keys(long B, unsigned long long* keys, int64_t* ids, long ld_ids, int64_t* pos, int64_t end_id,
                          int64_t pad_id, int* finished, int* n_finished, void* stream);
 
@@ -382,10 +385,13 @@ typedef struct {
   void* cache;
   long c_row, c_batch, kv_col0;
   const int64_t* pos;
-  /* argmax_keys (u64 [M], NULL: off): the greedy pick folded into the vocabulary head. Each row's
-   * maximum over the N columns of act(A . B^T + bias) leaves as one atomic max of
+  /* argmax_keys (u64 [MIT_ARGMAX_SLOTS][M], NULL: off): the greedy pick folded into the vocabulary head.
+   * Each 64-column block's maximum of row m over act(A . B^T + bias) leaves as one atomic max of
    * ord(value) << 32 | (0xFFFFFFFF - column) (ord: the order-preserving u32 image of an f32, NaN
-   * largest), so the surviving key is the first maximal column (torch.argmax). bf16 A rows, no residual
+   * largest) into slot (column block % MIT_ARGMAX_SLOTS) of the row, so the largest key over the row's
+   * slots is its first maximal column (torch.argmax). The slots spread the atomics: with one key per
+   * row all 157 column blocks of a 10000-word head hit the same 32 cache lines of 256 rows' keys, and the
+   * memory-side atomics on them serialised the launch (~29 us per token step). bf16 A rows, no residual
    * or activation; C / z_out may be NULL. The keys must be 0 before the launch (mit_greedy_pick_keys
    * leaves them 0). N need not be a multiple of 8 in this mode (any vocabulary: columns >= N never
    * enter the maximum). */

@@ -651,7 +651,7 @@ __global__ __launch_bounds__(NW * 64) void decode_gemm_kernel(mit_decode_gemm_ar
                          (uint32_t)__shfl_xor((int)(uint32_t)best, x, 64);
       best = o > best ? o : best;
     }
-    if (rok && (tid % TPR) == 0) atomicMax(g.argmax_keys + gr, (unsigned long long)best);
+    if (rok && (tid % TPR) == 0) atomicMax(g.argmax_keys + (bn % MIT_ARGMAX_SLOTS) * M + gr, (unsigned long long)best);
     return;
   }
   if (g.stats_out) {  // this tile's (mean, M2) per row over its valid columns; TPR lanes per row
@@ -844,16 +844,22 @@ extern "C" int mit_greedy_pick(long B, long V, const float* logits, long ld, int
   return MIT_OK;
 }
 
-// one block: row b's pick from the head's argmax key, the key reset, then *pos += 1 once every row has
-// read the old position (the __syncthreads orders the block's reads before thread 0's write)
+// one block: row b's pick from the largest of its head argmax slot keys, the keys reset, then *pos += 1 once
+// every row has read the old position (the __syncthreads orders the block's reads before thread 0's write)
 __global__ __launch_bounds__(1024) void greedy_pick_keys_kernel(long B, unsigned long long* __restrict__ keys,
                                                                 int64_t* __restrict__ ids, long ld_ids, int64_t* pos,
                                                                 int64_t end_id, int64_t pad_id, int* __restrict__ finished,
                                                                 int* __restrict__ n_finished) {
   const long p = *pos;
   for (long b = threadIdx.x; b < B; b += blockDim.x) {
-    const unsigned long long k = keys[b];
-    keys[b] = 0ull;
+    unsigned long long k = 0ull;
+#pragma unroll
+    for (int sl = 0; sl < MIT_ARGMAX_SLOTS; ++sl) {
+      const unsigned long long ks = keys[sl * B + b];
+      k = ks > k ? ks : k;
+    }
+#pragma unroll
+    for (int sl = 0; sl < MIT_ARGMAX_SLOTS; ++sl) keys[sl * B + b] = 0ull;
     const int64_t bi = (int64_t)(0xFFFFFFFFu - (uint32_t)k);
     if (finished[b]) {
       ids[b * ld_ids + p + 1] = pad_id;

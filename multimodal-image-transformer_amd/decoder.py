@@ -285,7 +285,8 @@ class DecodeState:
             self.z = [torch.empty(B, d, dtype=torch.float32, device=dev) for _ in range(3)]
             self.zst = [torch.empty(B, P, 2, dtype=torch.float32, device=dev) for _ in range(3)]
             self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.keys = torch.zeros(B, dtype=torch.int64, device=dev)  # the head's packed argmax (0 between steps)
+            # the head's packed argmax, ARGMAX_SLOTS per row (0 between steps)
+            self.keys = torch.zeros(native.ARGMAX_SLOTS * B, dtype=torch.int64, device=dev)
 
     def token_lists(self) -> List[List[int]]:
         """Per row: START .. up to and including the first END (model.py:236-242), else max_len ids."""

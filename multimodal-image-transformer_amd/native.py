@@ -28,6 +28,7 @@ from torch.utils._python_dispatch import TorchDispatchMode
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MIT_HIP_LIB", os.path.join(_HERE, "lib", "libmit_hip.so"))
 ABI_VERSION = 6  # mit_abi_version() of the library this binding matches (include/mit_hip.h)
+ARGMAX_SLOTS = 16  # MIT_ARGMAX_SLOTS: slots per row of the decode head's argmax keys
 
 F32, BF16 = 0, 1
 K_CONTIG, MN_CONTIG = 0, 1
@@ -761,9 +762,11 @@ def decode_gemm(a, w, *, out=None, bias=None, act=ACT_NONE, a_ln=None, residual=
     residual: bf16 rows, or f32 pre-LN sums when r_ln = (stats, gamma, beta) (+ LN(residual));
     z_out / stats_out: f32 pre-LN sum of the next LayerNorm and its per-64-column row statistics
     [M, ceil(N/64), 2]; cache: the columns >= kv_col0 also go to cache[m*c_batch + pos*c_row + n - kv_col0];
-    argmax_keys: int64 [M] zeros <- each row's packed (value, first column) maximum (the greedy pick
-    folded into the head: greedy_pick_keys)."""
+    argmax_keys: int64 [ARGMAX_SLOTS * M] zeros <- per row and slot the packed (value, first column) maximum
+    of the column blocks of that slot (the greedy pick folded into the head: greedy_pick_keys, argmax_of_keys)."""
     M, K = a.shape[0], a.shape[-1]
+    if argmax_keys is not None and argmax_keys.numel() < ARGMAX_SLOTS * M:
+        raise NativeError(f"decode_gemm: argmax_keys needs {ARGMAX_SLOTS} x M = {ARGMAX_SLOTS * M} entries")
     N = w.shape[0]
     r_mode = 0 if residual is None else (2 if r_ln is not None else 1)
     g = DecodeGemmArgs(M, N, K, ptr(a), a.stride(0), ptr(a_ln[0]) if a_ln else None, ptr(a_ln[1]) if a_ln else None,
@@ -779,9 +782,19 @@ def decode_gemm(a, w, *, out=None, bias=None, act=ACT_NONE, a_ln=None, residual=
 
 def greedy_pick_keys(keys, ids, pos, end_id, pad_id, finished, n_finished):
     """ids[:, pos + 1] <- the picks a decode_gemm(argmax_keys=keys) left (keys reset to 0), then pos += 1."""
-    B = keys.shape[0]
+    B = ids.shape[0]
+    if keys.numel() != ARGMAX_SLOTS * B:
+        raise NativeError(f"greedy_pick_keys: keys must hold {ARGMAX_SLOTS} x B = {ARGMAX_SLOTS * B} entries")
     _check(lib().mit_greedy_pick_keys(B, ptr(keys), ptr(ids), ids.shape[1], ptr(pos), int(end_id), int(pad_id),
                                       ptr(finished), ptr(n_finished), stream_ptr()), "mit_greedy_pick_keys")
+
+
+def argmax_of_keys(keys, M):
+    """The column each row's argmax keys (int64 [ARGMAX_SLOTS * M], unsigned packed keys) name: the largest
+    key over the row's slots, unsigned order (host-side helper for tests and tools)."""
+    k = keys.view(ARGMAX_SLOTS, M) ^ torch.iinfo(torch.int64).min  # unsigned order as signed order
+    best = k.max(0).values ^ torch.iinfo(torch.int64).min
+    return 0xFFFFFFFF - (best & 0xFFFFFFFF)
 
 
 def decode_layernorm(z, stats, gamma, beta, out, eps=1e-5):

@@ -384,7 +384,7 @@ def test_decode_gemm_argmax_keys_exact():
     a = torch.randint(-2, 3, (M, K), generator=g).to(dev, torch.bfloat16)
     w = torch.randint(-2, 3, (V, K), generator=g).to(dev, torch.bfloat16)
     ref = a.double() @ w.double().t()
-    keys = torch.zeros(M, dtype=torch.int64, device=dev)
+    keys = torch.zeros(N.ARGMAX_SLOTS * M, dtype=torch.int64, device=dev)
     for case in range(3):
         bias = torch.randint(-4, 5, (V,), generator=g).float()
         if case == 1:  # a tie in every row: columns 123 and 4000 dominate equally -> 123
@@ -396,7 +396,7 @@ def test_decode_gemm_argmax_keys_exact():
         bias = bias.to(dev)
         N.decode_gemm(a, w, bias=bias, argmax_keys=keys)
         want = (ref + bias.double()).argmax(1)
-        got = 0xFFFFFFFF - (keys & 0xFFFFFFFF)
+        got = N.argmax_of_keys(keys, M)
         assert torch.equal(got, want), (case, (got != want).sum().item())
         if case == 1:
             assert (want == 123).all()
@@ -426,10 +426,10 @@ def test_decode_gemm_argmax_keys_ragged_vocab(V):
     w = wp[:V]
     bias = torch.randint(-4, 5, (V + 8,), generator=g).float().to(dev)
     bias[V:] = 1e4
-    keys = torch.zeros(M, dtype=torch.int64, device=dev)
+    keys = torch.zeros(N.ARGMAX_SLOTS * M, dtype=torch.int64, device=dev)
     N.decode_gemm(a, w, bias=bias[:V], argmax_keys=keys)
     want = (a.double() @ w.double().t() + bias[:V].double()).argmax(1)
-    got = 0xFFFFFFFF - (keys & 0xFFFFFFFF)
+    got = N.argmax_of_keys(keys, M)
     assert torch.equal(got, want)
 
 
@@ -437,7 +437,7 @@ def test_decode_gemm_argmax_keys_rejects_outputs():
     dev = torch.device("cuda")
     a = torch.zeros(4, 64, device=dev, dtype=torch.bfloat16)
     w = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
-    keys = torch.zeros(4, dtype=torch.int64, device=dev)
+    keys = torch.zeros(N.ARGMAX_SLOTS * 4, dtype=torch.int64, device=dev)
     with pytest.raises(N.NativeError, match="argmax_keys"):
         N.decode_gemm(a, w, out=torch.empty(4, 64, device=dev, dtype=torch.bfloat16), argmax_keys=keys)
     with pytest.raises(N.NativeError, match="argmax_keys"):

@@ -203,7 +203,8 @@ def _attn_ref(q, k, v, causal, kpm, scale, drop=None):
 
 
 _HD_CASES = [(64, k) for k in ["self_causal_pad", "cross", "bidir", "cross_s1", "self_drop", "self_long", "cross577",
-                                "cross_drop", "bidir577", "bidir150", "cross230", "cross_drop40", "cross256", "cross_drop17"]]
+                                "cross_drop", "bidir577", "bidir150", "cross230", "cross_drop40", "cross256", "cross_drop17",
+                                "cross_q20", "cross_q20_drop"]]
 # other head dims (generic kernels): configs[0]'s decoder is d128 / 8 heads = head_dim 16
 _HD_CASES += [(hd, k) for hd in (16, 32, 128) for k in ["self_causal_pad", "cross", "self_drop", "cross_s1"]]
 
@@ -237,10 +238,13 @@ def test_attention_fwd_bwd(dtype, D, kind):
         Lq, Lk = 50, 256
     elif kind == "cross_drop17":
         Lq, Lk = 63, 17
+    # two query tiles over 5 key units (4 chunks + a 48-key tail): the head kernel's key split in 4 parts
+    elif kind in ("cross_q20", "cross_q20_drop"):
+        Lq, Lk = 20, 300
     else:
         Lq = Lk = 197
     causal = kind.startswith("self")
-    drop_p = 0.1 if kind in ("self_drop", "cross_drop", "cross_drop40", "cross_drop17") else 0.0
+    drop_p = 0.1 if kind in ("self_drop", "cross_drop", "cross_drop40", "cross_drop17", "cross_q20_drop") else 0.0
     q = torch.randn(B, Lq, H * D, device=dev()).to(dtype)
     kv = torch.randn(B, Lk, 2 * H * D, device=dev()).to(dtype)
     k, v = kv[..., :H * D], kv[..., H * D:]

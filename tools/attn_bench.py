@@ -10,20 +10,28 @@ import torch  # noqa: E402
 
 import native  # noqa: E402
 
-SHAPES = [("enc vit-b16", 64, 12, 197, 197), ("dec cross", 64, 8, 63, 197), ("enc clip-l336", 16, 16, 577, 577)]
+SHAPES = [("enc vit-b16", 64, 12, 197, 197), ("dec cross", 64, 8, 63, 197), ("enc clip-l336", 16, 16, 577, 577),
+          # the decoder cross-attention as trained (dropout 0.1) at configs[1] / [3] / [2] memory lengths
+          ("dec cross drop", 64, 8, 63, 197, 0.1), ("cfg3 cross drop", 64, 12, 63, 257, 0.1),
+          ("cfg2 cross drop", 64, 8, 63, 577, 0.1), ("cfg2 cross", 64, 8, 63, 577)]
 
 
 def run(iters=20):
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(0)
-    for name, B, H, Lq, Lk in SHAPES:
+    seed = torch.tensor([5], dtype=torch.int64, device=dev)
+    only = os.environ.get("ATTN_SHAPES")
+    for name, B, H, Lq, Lk, *drop in SHAPES:
+        if only and name not in only.split(","):
+            continue
         E = H * 64
         qkv = torch.randn(B, max(Lq, Lk), 3 * E, generator=g).to(dev, torch.bfloat16)
         o = torch.empty(B, Lq, E, device=dev, dtype=torch.bfloat16)
         lse = torch.empty(B * H * Lq, device=dev)
         T = max(Lq, Lk)
         a = native.attn_args(qkv, 3 * E, T * 3 * E, qkv[..., E:], 3 * E, T * 3 * E, qkv[..., 2 * E:], 3 * E, T * 3 * E,
-                             o, E, Lq * E, lse=lse, scale=0.125)
+                             o, E, Lq * E, lse=lse, scale=0.125, drop_p=drop[0] if drop else 0.0,
+                             seed=seed if drop else None, site=3)
         for _ in range(3):
             native.attention_fwd(native.BF16, B, H, Lq, Lk, a)
         torch.cuda.synchronize()

@@ -13,7 +13,8 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r04}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-ARGS="--no-cpu-baseline --no-also --steps 10 --warmup 3"
+# WORKLOAD=clip336 / cfg3: the same passes over that workload (bench.py --workload)
+ARGS="--no-cpu-baseline --no-also --steps 10 --warmup 3${WORKLOAD:+ --workload $WORKLOAD}"
 P="rocprofv3 --output-format rocpd csv"
 timeout -k 10 300 $P --kernel-trace --stats -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.json 2> $OUT/trace.err &&
 timeout -k 10 300 $P --kernel-trace --stats -d $OUT/trace_noprefetch -o run -- python3 bench.py $ARGS --no-prefetch --no-roofline > $OUT/trace_noprefetch.json 2> $OUT/trace_noprefetch.err &&
