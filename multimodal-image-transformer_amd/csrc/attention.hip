@@ -500,18 +500,9 @@ __device__ __forceinline__ float max16(const float (&s)[16]) {
 }
 constexpr bf16x8 ones8 = {(bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f, (bf16)1.0f};
 
-// ks > 1 (key split; the decoder's cross-attention: <= 4 query tiles against 197-577 keys): wave w sweeps
-// query tile w % nqt over the ks-th part w / nqt of the head's 64-key chunks (the 16-key tail goes with
-// the last part), and the parts' (m, l, O) merge through LDS once every wave's sweep is done. Without the
-// split such a head ran 4 waves per workgroup, each a dependent chain over all the keys (configs[2]'s
-// S = 577 cross-attention: 4.4 % MFMA-busy, 1.8 TB/s; profiles/r06_clip336_pmc.json).
-// SPLIT is a template flag: the unsplit instances (the encoders' MHSA) keep their registers (122 / 132
-// VGPRs; the split bookkeeping in them spilled 13 / 23), and the split ones run <= 8 waves (at 16 waves,
-// 128 VGPRs, they spilled 13 / 24).
-constexpr int KS_SLOT = 18 * 64 * 4;  // LDS bytes per merged part: O^T (16 floats) + m + l per lane
-template <bool DROP, bool SPLIT>
-__global__ __attribute__((amdgpu_flat_work_group_size(64, (DROP || SPLIT) ? 512 : 1024))) void attn_fwd_head(
-    long H, long Lq, long Lk, AttnK a, int kbytes, int vbytes, int lkp, int ks) {
+template <bool DROP>
+__global__ __attribute__((amdgpu_flat_work_group_size(64, DROP ? 512 : 1024))) void attn_fwd_head(long H, long Lq, long Lk, AttnK a, int kbytes, int vbytes,
+                                                      int lkp) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* Ks = lds;
   char* Vs = lds + (long)lkp * 128;
@@ -562,11 +553,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, (DROP || SPLIT) ? 512 
     vofs[i][0] = koff_v(g * 4 + q, colb);
     vofs[i][1] = koff_v(16 + g * 4 + q, colb);
   }
-  const int nfull = lkp >> 6, nunits = nfull + ((lkp & 63) ? 1 : 0);  // 64-key chunks (+ the tail)
-  const int sp = SPLIT ? w / nqt : 0;
-  const int u0 = SPLIT ? sp * nunits / ks : 0, u1 = SPLIT ? (sp + 1) * nunits / ks : nunits;  // chunks [u0, u1)
-  MIT_DASSERT(!SPLIT || (nw == nqt * ks && ks <= nunits));
-  for (int qt = SPLIT ? w % nqt : w; qt < nqt; qt += nw) {
+  for (int qt = w; qt < nqt; qt += nw) {
     const long qi = (long)qt * 16 + (lane & 15);
     const bool qlive = qi < Lq;
     bf16x8 qf[2];
@@ -587,12 +574,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, (DROP || SPLIT) ? 512 
     for (int i = 0; i < 4; ++i) ot[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, l = 0.f;
     f32x4 lacc = {0.f, 0.f, 0.f, 0.f};  // MFMA-accumulated denominator of the full chunks (!DROP)
-    const char* Kc = Ks + (SPLIT ? u0 * 64 * 128 : 0);
-    const char* Vc = Vs + (SPLIT ? u0 * 64 * 128 : 0);
-    int j0 = SPLIT ? u0 * 64 : 0;
+    const char* Kc = Ks;
+    const char* Vc = Vs;
+    int j0 = 0;
     const int ilk = (int)Lk;
-    const int jend = SPLIT ? min(u1, nfull) * 64 : lkp - 63;
-    for (; j0 < jend; j0 += 64, Kc += 64 * 128, Vc += 64 * 128) {
+    for (; j0 + 64 <= lkp; j0 += 64, Kc += 64 * 128, Vc += 64 * 128) {
       // ---- S^T = K Q^T for keys j0 .. j0+63 (4 key tiles of 16) ----
       f32x4 st[4];
 #pragma unroll
@@ -673,7 +659,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, (DROP || SPLIT) ? 512 
     }
     if (!DROP) l += lacc[0];
     // ---- tail: the last 16 / 32 / 48 keys (K/V are staged to a multiple of 16 rows, not 64) ----
-    const int ntail = (!SPLIT || u1 > nfull) ? (lkp - j0) >> 4 : 0;  // wave-uniform
+    const int ntail = (lkp - j0) >> 4;  // wave-uniform
     if (ntail) {
       f32x4 st[3];
       float s[12];
@@ -738,32 +724,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, (DROP || SPLIT) ? 512 
           const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Vc + voff + vofs[i][0]));
           ot[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(lo, __builtin_bit_cast(s16x4, pq), ot[i], 0, 0, 0);
         }
-      }
-    }
-    if constexpr (SPLIT) {  // merge the key parts of this query tile: parts 1 .. ks-1 hand (m, l, O^T) to part 0
-      __syncthreads();  // every wave's K/V reads are done: the merge reuses the LDS
-      float* slot = (float*)(lds + (long)((sp - 1) * nqt + qt) * KS_SLOT);
-      if (sp > 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int t = 0; t < 4; ++t) slot[(i * 4 + t) * 64 + lane] = ot[i][t];
-        slot[16 * 64 + lane] = m;
-        slot[17 * 64 + lane] = l;
-      }
-      __syncthreads();
-      if (sp > 0) return;
-      for (int pt = 1; pt < ks; ++pt) {
-        const float* o2 = (const float*)(lds + (long)((pt - 1) * nqt + qt) * KS_SLOT);
-        const float m2 = o2[16 * 64 + lane], l2 = o2[17 * 64 + lane];
-        const float mn = __builtin_fmaxf(m, m2);  // finite: every part holds live keys
-        const float a1 = __builtin_amdgcn_exp2f(m - mn), a2 = __builtin_amdgcn_exp2f(m2 - mn);
-        l = l * a1 + l2 * a2;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int t = 0; t < 4; ++t) ot[i][t] = ot[i][t] * a1 + o2[(i * 4 + t) * 64 + lane] * a2;
-        m = mn;
       }
     }
     if (qlive) {
@@ -1238,11 +1198,6 @@ AttnK make_k(const mit_attn_args* x) {
 
 // dropout calls with B*H*Lq*Lk at or past this run the 64-bit mask-index kernels (mit_attention_set_index_limit)
 static double g_idx32_limit = 4294967296.0;
-// key-split parts per head for attn_fwd_head (MIT_ATTN_KSPLIT, an A/B knob while it is measured)
-static int g_attn_ksplit = [] {
-  const char* e = getenv("MIT_ATTN_KSPLIT");
-  return e ? std::max(1, atoi(e)) : 4;
-}();
 extern "C" int mit_attention_set_index_limit(double limit) {
   g_idx32_limit = limit > 0 ? limit : 4294967296.0;
   return MIT_OK;
@@ -1284,37 +1239,21 @@ extern "C" int mit_attention_fwd(int dtype, long B, long H, long Lq, long Lk, lo
       // in one workgroup per CU; ViT-B/16: 13 = 8 + 5 in two) rather than fewer balanced waves (13 + 13 + 11,
       // 7 + 6): more waves to hide the sweep's latency, 47.2 -> 45.2 / 26.7 -> 26.5 us, configs[2]
       // 2067 -> 2078 pairs/s (profiles/r05_decoder_experiments.txt)
-      // key split (attn_fwd_head ks): a head of <= 4 query tiles (the decoder's cross-attention) on up to 8
-      // waves, nqt per 64-key chunk range
-      const int nunits = lkp / 64 + (lkp % 64 ? 1 : 0);
-      int ks = 1;
-      if (nqt <= 4 && nunits >= 2) ks = std::min(nunits, std::min(g_attn_ksplit, 8 / nqt));
-      const int nw = ks > 1 ? nqt * ks : std::min(nqt, maxw);
-      const int lds = std::max(lkp * 256, ks > 1 ? (ks - 1) * nqt * KS_SLOT : 0);
+      const int nw = std::min(nqt, maxw);
+      const int lds = lkp * 256;
       static bool attr = false;
       if (!attr) {
-        (void)hipFuncSetAttribute((const void*)attn_fwd_head<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)attn_fwd_head<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   HK_MAX * 256);
-        (void)hipFuncSetAttribute((const void*)attn_fwd_head<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  HK_MAX * 256);
-        (void)hipFuncSetAttribute((const void*)attn_fwd_head<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  HK_MAX * 256);
-        (void)hipFuncSetAttribute((const void*)attn_fwd_head<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)attn_fwd_head<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   HK_MAX * 256);
         attr = true;
       }
       dim3 hg((unsigned)H, (unsigned)B);
-      if (a.dropout) {
-        if (ks > 1)
-          hipLaunchKernelGGL((attn_fwd_head<true, true>), hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp, ks);
-        else
-          hipLaunchKernelGGL((attn_fwd_head<true, false>), hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp, 1);
-      } else {
-        if (ks > 1)
-          hipLaunchKernelGGL((attn_fwd_head<false, true>), hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp, ks);
-        else
-          hipLaunchKernelGGL((attn_fwd_head<false, false>), hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp, 1);
-      }
+      if (a.dropout)
+        hipLaunchKernelGGL(attn_fwd_head<true>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
+      else
+        hipLaunchKernelGGL(attn_fwd_head<false>, hg, dim3(64 * nw), lds, s, H, Lq, Lk, a, (int)kb, (int)vb, lkp);
     } else if (!a.dropout || (double)B * (double)H * (double)Lq * (double)Lk < g_idx32_limit) {
       hipLaunchKernelGGL(attn_fwd_mfma, grid, dim3(256), 0, s, H, Lq, Lk, a, (int)kb, (int)vb);
     } else {  // dropout indices past 2^32 (the MFMA kernels form them in 32 bits)
