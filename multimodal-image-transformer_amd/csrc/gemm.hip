@@ -116,7 +116,7 @@ __device__ __forceinline__ void epi8(const Epi& e, void* C, long ldc, long N, lo
       v[k + 1] = r[1];
     }
   } else if (ACT == MIT_ACT_QUICK_GELU) {
-    quick_gelu_n<8>(v);
+    quick_gelu_fast_n<8>(v);
   } else if (ACT != MIT_ACT_NONE) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = act_apply<ACT, true>(e.act, v[k]);
@@ -211,7 +211,7 @@ __device__ __forceinline__ void epi8x(const Epi& e, void* C, long ldc, long N, l
       v[k + 1] = g[1];
     }
   } else if (ACT == MIT_ACT_QUICK_GELU) {
-    quick_gelu_n<8>(v);
+    quick_gelu_fast_n<8>(v);
   } else if (ACT != MIT_ACT_NONE) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = act_apply<ACT, true>(e.act, v[k]);
@@ -781,7 +781,7 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
             v[t + 1] = q[1];
           }
         } else if (ACT == MIT_ACT_QUICK_GELU) {
-          quick_gelu_n<4>(v);
+          quick_gelu_fast_n<4>(v);
         } else if (ACT != MIT_ACT_NONE) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) v[t] = act_apply<ACT, true>(e.act, v[t]);

@@ -550,6 +550,9 @@ class TransformerDecoder:
                 A.gws_kv = torch.empty((native.gemm_grouped_ws_bytes([kv_prob]) + 255) // 4, dtype=torch.float32,
                                        device=self.device)
             side.run(lambda: native.gemm_grouped([kv_prob], A.gws_kv), reads=(A.dkv,))
+            # its own DP bucket (12.6 MB at cfg1): all-reduced under the rest of the backward instead of with
+            # the embedding / projection gradients after it (exposed communication)
+            ready("cross_kv.weight", "cross_kv.bias")
         for l in reversed(range(L)):
             if tick is not None:
                 tick()
@@ -639,7 +642,7 @@ class TransformerDecoder:
             native.gemm(A.dkv, w("cross_kv.weight"), A.dmem, BS, d, L * 2 * d, b_layout=MN, ldb=d, workspace=ws)
             dW(A.dmem, enc_rows, "projection.weight", "projection.bias", d, E, BS, d, enc_ld)
             last = "projection.bias"
-        ready("cross_kv.weight", last)
+        ready("token_embedding.weight" if early else "cross_kv.weight", last)
         if side is not None:
             side.join()
 

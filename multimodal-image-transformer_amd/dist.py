@@ -57,6 +57,8 @@ class DataParallel:
         self.overlap = overlap
         self._work: List = []
         self._pending_spans = []
+        self._covered = []  # the spans announced this step: every entry in exactly one (checked on 4 steps)
+        self._checks_left = 4
         self._broadcast_state()
 
     def _broadcast_state(self):
@@ -75,6 +77,7 @@ class DataParallel:
 
     def grads_ready(self, first: str, last: str):
         s, e = self.store.span(first, last)
+        self._covered.append((s, e))
         if self.overlap:
             self._work.append(dist.all_reduce(self.store.grad[s:e], group=self.group, async_op=True))
         else:
@@ -84,6 +87,15 @@ class DataParallel:
         native.host_call(lambda: self._finish(loss))
 
     def _finish(self, loss: torch.Tensor):
+        spans, self._covered = sorted(self._covered), []
+        # host-side bookkeeping only, on the first steps (the buckets are the same every step): every parameter
+        # entry in exactly one bucket (a missed or doubly reduced entry would leave the ranks' gradients unequal
+        # or scaled); the gaps between entries are alignment
+        self._checks_left -= 1
+        for name, (_, off, n) in (self.store.index.items() if self._checks_left >= 0 else ()):
+            hits = sum(1 for a, b in spans if a <= off and off + n <= b)
+            if hits != 1:
+                raise RuntimeError(f"DataParallel: gradient entry {name} is in {hits} buckets this step ({spans})")
         if not self.overlap and self._pending_spans:
             s = min(a for a, _ in self._pending_spans)
             e = max(b for _, b in self._pending_spans)
