@@ -34,7 +34,20 @@ def main(iters=200):
     }
     wshape = {"out-proj +res-LN (N 512, K 512)": (d, d), "cross-q LN-operand (N 512, K 512)": (d, d),
               "linear1 LN+relu (N 2048, K 512)": (F, d), "linear2 +res-LN (N 512, K 2048)": (d, F)}
+    # the vocabulary head (V = 10000): the folded greedy argmax vs a plain bf16 output, and mit_gemm's kernel
+    V = 10000
+    keys = torch.zeros(native.ARGMAX_SLOTS * M, dtype=torch.int64, device=dev)
+    bv = torch.zeros(V, device=dev)
+    lg = torch.empty(M, V, device=dev, dtype=torch.bfloat16)
+    shapes["head argmax_keys (N 10000, K 512)"] = lambda w: native.decode_gemm(a16, w, bias=bv, argmax_keys=keys)
+    shapes["head bf16 out (N 10000, K 512)"] = lambda w: native.decode_gemm(a16, w, out=lg, bias=bv)
+    shapes["head mit_gemm bf16 (N 10000, K 512)"] = lambda w: native.gemm(a16, w, lg, M, V, d, bias=bv)
+    for k in ("head argmax_keys (N 10000, K 512)", "head bf16 out (N 10000, K 512)", "head mit_gemm bf16 (N 10000, K 512)"):
+        wshape[k] = (V, d)
+    only = os.environ.get("DG_SHAPES")
     for name, fn in shapes.items():
+        if only and not any(o in name for o in only.split(",")):
+            continue
         ws = [bf(*wshape[name]) for _ in range(12)]
         for mode in ("warm", "12 weights"):
             for i in range(10):
