@@ -121,6 +121,13 @@ typedef struct {
    * caller whose other stream runs beside this launch, so a partial last round is not left idle
    * (encoder.forward_iter_groups); 128 = the 128x128 kernel. mit_gemm_set_variant 1 / 2 / 3 override it. */
   int tiles;
+  /* argmax_keys (u64 [MIT_ARGMAX_SLOTS][M], NULL: off): the greedy pick folded into a vocabulary head, as
+   * mit_decode_gemm_args.argmax_keys (same packed keys, slot = 128-column block % MIT_ARGMAX_SLOTS; C may be
+   * NULL and is not written). bf16 NT operands, bias only (no activation, residual, aux, dropout, alpha 1; the
+   * bias is read in 8-float vectors up to round8(N));
+   * runs on the 128x128 kernel: the batched decode's head (M = 256, N = V) in one round of 158 blocks, 9-10 us,
+   * against 20 us for mit_decode_gemm's 628 split-K 64x64 blocks at one per CU. */
+  unsigned long long* argmax_keys;
 } mit_gemm_args;
 int mit_gemm(const mit_gemm_args* args, void* stream);
 long mit_gemm_workspace_bytes(long M, long N, long K);

@@ -63,7 +63,17 @@ struct Epi {
   float ln_eps;
   // per-64-column (mean, M2) of each output row (256 kernel, STG 4): stats_out [M][N / 64][2]
   float* stats_out;
+  // the greedy argmax of each row folded in (128 kernel, gathered epilogue): keys [MIT_ARGMAX_SLOTS][M]
+  unsigned long long* argmax_keys;
 };
+
+// ord(v) << 32 | (0xFFFFFFFF - column): the order of (value, first column) as one u64, NaN largest
+// (mit_decode_gemm's argmax keys, decode.hip)
+__device__ __forceinline__ uint64_t argmax_key(float v, long col) {
+  const uint32_t u = __float_as_uint(v);
+  const uint32_t o = v != v ? 0xFFFFFFFFu : ((u & 0x80000000u) ? ~u : (u | 0x80000000u));
+  return ((uint64_t)o << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)col);
+}
 
 constexpr int ACT_RT = -1;
   // activation read from Epi::act at run time (generic instance)
@@ -411,6 +421,27 @@ __device__ __forceinline__ void gemm_bf16_body(const bf16* __restrict__ A, const
     for (int pass = 0; pass < NP; ++pass) xs[pass] = epi_x8(e, M, N, m0 + ((pass * NT + tid) >> 4), gc);
     gather_wait();
     const uint64_t key = epi_key<DROP>(e);
+    if (ACT == MIT_ACT_NONE && !DROP && e.argmax_keys) {  // the rows' argmax over this tile's 128 columns
+#pragma unroll
+      for (int pass = 0; pass < NP; ++pass) {
+        const int r = (pass * NT + tid) >> 4, c8 = (tid & 15) * 8;
+        const long gr = m0 + r;
+        uint64_t best = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t kk = argmax_key(cs[r * CST + c8 + k] + b[k], gc + k);
+          if (gc + k < N && kk > best) best = kk;
+        }
+#pragma unroll
+        for (int x = 1; x < 16; x <<= 1) {  // the row's 16 lanes (tid & 15)
+          const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor((int)(best >> 32), x, 64) << 32) |
+                             (uint32_t)__shfl_xor((int)(uint32_t)best, x, 64);
+          best = o > best ? o : best;
+        }
+        if ((tid & 15) == 0 && gr < M) atomicMax(e.argmax_keys + (long)(bn % MIT_ARGMAX_SLOTS) * M + gr, (unsigned long long)best);
+      }
+      return;
+    }
 #pragma unroll
     for (int pass = 0; pass < NP; ++pass) {
       const int r = (pass * NT + tid) >> 4, c8 = (tid & 15) * 8;
@@ -1656,6 +1687,7 @@ extern "C" int mit_gemm_plan(const mit_gemm_args* g, int* ksplit) {
   if (ksplit) *ksplit = 1;
   if (!g || g->M <= 0 || g->N <= 0) return 0;
   if (g->dtype != MIT_BF16) return 64;
+  if (g->argmax_keys) return 128;
   const Split sp = plan_split(g);
   if (ksplit) *ksplit = sp.ks;
   if (sp.ks == 1 && use_rs(g)) return 65;  // the 64x64 register-streaming kernel
@@ -1669,7 +1701,7 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   MIT_RECORD([c = *g, stream]() { return mit_gemm(&c, stream); });
   MIT_CHECK_ARG(g->dtype == MIT_F32 || g->dtype == MIT_BF16, "mit_gemm: bad dtype %d", g->dtype);
   MIT_CHECK_ARG(g->M >= 0 && g->N >= 0 && g->K >= 0, "mit_gemm: negative extent");
-  MIT_CHECK_ARG(g->A && g->B && g->C, "mit_gemm: null operand");
+  MIT_CHECK_ARG(g->A && g->B && (g->C || g->argmax_keys), "mit_gemm: null operand");
   MIT_CHECK_ARG(g->a_layout == MIT_K_CONTIG || g->a_layout == MIT_MN_CONTIG, "mit_gemm: bad a_layout");
   MIT_CHECK_ARG(g->b_layout == MIT_K_CONTIG || g->b_layout == MIT_MN_CONTIG, "mit_gemm: bad b_layout");
   MIT_CHECK_ARG(g->act >= MIT_ACT_NONE && g->act <= MIT_ACT_QUICK_GELU, "mit_gemm: bad act %d", g->act);
@@ -1693,6 +1725,13 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
     b_bytes = 2 * (g->b_layout == MIT_K_CONTIG ? (g->N - 1) * g->ldb + g->K : (g->K - 1) * g->ldb + g->N);
     if (g->K == 0) a_bytes = b_bytes = 0;
     MIT_CHECK_ARG(a_bytes < (1L << 31) && b_bytes < (1L << 31), "mit_gemm(bf16): operand spans >= 2 GiB");
+  }
+  if (g->argmax_keys) {
+    MIT_CHECK_ARG(g->dtype == MIT_BF16 && g->a_layout == MIT_K_CONTIG && g->b_layout == MIT_K_CONTIG && !g->C &&
+                      g->act == MIT_ACT_NONE && !g->residual && !g->aux && g->drop_p <= 0.f && g->alpha == 1.0f &&
+                      !g->rowsum && !g->accumulate && !g->ln_stats && !g->stats_out && (!g->bias || al16(g->bias)) &&
+                      ((uintptr_t)g->argmax_keys % 8) == 0 && g->N < (1L << 32),
+                  "mit_gemm: argmax_keys needs bf16 NT operands, a bias only and no C");
   }
   if (g->ln_stats || g->stats_out) {
     // the LayerNorm fold / row statistics exist only in the 256 kernel's LDS-staged bf16 epilogue
@@ -1734,7 +1773,14 @@ extern "C" int mit_gemm(const mit_gemm_args* g, void* stream) {
   e.dscale = g->drop_p < 1.0f ? 1.0f / (1.0f - g->drop_p) : 0.0f;
   e.vec = (g->N % 8 == 0) && (g->ldc % 8 == 0) && al16(g->C) && (!g->bias || al16(g->bias)) &&
           (!g->residual || (g->ldr % 8 == 0 && al16(g->residual))) && (!g->aux || (g->ld_aux % 8 == 0 && al16(g->aux)));
+  e.argmax_keys = g->argmax_keys;
   hipStream_t s = (hipStream_t)stream;
+  if (g->argmax_keys) {  // the 128 kernel's gathered epilogue (any N: columns >= N never enter a key)
+    e.vec = 1;
+    launch_bf16<MIT_K_CONTIG, MIT_K_CONTIG, MIT_ACT_NONE, false>(g, e, (int)a_bytes, (int)b_bytes, Split{}, s);
+    MIT_LAUNCH_CHECK("mit_gemm");
+    return MIT_OK;
+  }
   if (g->dtype == MIT_BF16) {
     const int ab = (int)a_bytes, bb = (int)b_bytes;
     const Split sp = plan_split(g);

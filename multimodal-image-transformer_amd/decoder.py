@@ -799,7 +799,10 @@ class TransformerDecoder:
                                z_out=z3, stats_out=s3)
         q3 = f"layers.{L - 1}.norm3."
         native.decode_layernorm(z3, s3, p(q3 + "weight"), p(q3 + "bias"), stt.x)
-        native.decode_gemm(stt.x, w("fc_out.weight")[:V], bias=p("fc_out.bias")[:V], argmax_keys=stt.keys)
+        # the head on the 128x128 GEMM with the argmax epilogue (mit_gemm argmax_keys): one round of 158 blocks,
+        # ~10 us, against ~20 us for mit_decode_gemm's 628 split-K 64x64 blocks at one per CU
+        # (per token step, 3 interleaved processes on one box: 667 -> 658 us, 383.7 k -> 389.0 k tokens/s)
+        native.gemm(stt.x, w("fc_out.weight")[:V], None, B, V, d, bias=p("fc_out.bias")[:V], argmax_keys=stt.keys)
         native.greedy_pick_keys(stt.keys, stt.ids, stt.pos, stt.end_id, self.pad_idx, stt.finished, stt.n_finished)
 
     def forward_ops(self, tokens: torch.Tensor, mem: torch.Tensor, S: int, params: Dict[str, torch.Tensor],

@@ -54,7 +54,8 @@ class GemmArgs(ctypes.Structure):
                 ("bias", vp), ("act", I), ("residual", vp), ("ldr", L), ("aux", vp), ("ld_aux", L),
                 ("aux_scale", Fl), ("drop_p", Fl), ("seed", vp), ("site", U32), ("out_f32", I),
                 ("accumulate", I), ("rowsum", vp), ("workspace", vp), ("workspace_bytes", L),
-                ("ln_stats", vp), ("ln_colsum", vp), ("ln_parts", I), ("ln_eps", Fl), ("stats_out", vp), ("tiles", I)]
+                ("ln_stats", vp), ("ln_colsum", vp), ("ln_parts", I), ("ln_eps", Fl), ("stats_out", vp), ("tiles", I),
+                ("argmax_keys", vp)]
 
 
 class DecodeGemmArgs(ctypes.Structure):
@@ -417,8 +418,9 @@ def dtype_code(t: torch.Tensor) -> int:
 def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ldb=None, ldc=None, bias=None,
          act=ACT_NONE, residual=None, ldr=None, aux=None, ld_aux=None, aux_scale=1.0, alpha=1.0, drop_p=0.0,
          seed=None, site=0, accumulate=False, rowsum=None, workspace=None, ln_stats=None, ln_colsum=None, ln_eps=0.0,
-         stats_out=None, tiles=0):
+         stats_out=None, tiles=0, argmax_keys=None):
     """C = epi(alpha * A(m,k) B(k,n)); see include/mit_hip.h. Output dtype = C.dtype (f32 or operand dtype).
+    argmax_keys: int64 [ARGMAX_SLOTS * M] zeros <- the rows' packed argmax keys (argmax_of_keys); C may be None.
     rowsum: optional f32 [M] <- sum_k A(m,k) (fused bias gradient); workspace: split-K scratch, zero-filled
     once before first use (gemm_workspace(M, N, K)), one per stream. ln_stats / ln_colsum / ln_eps: the
     LayerNorm of A's rows folded in (B, bias already folded: encoder.fold_layernorm); stats_out: f32
@@ -427,9 +429,11 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
     dt = dtype_code(A)
     if B.dtype != A.dtype:
         raise NativeError("gemm: A and B dtypes differ")
-    if C.dtype != A.dtype and C.dtype != torch.float32:
+    if argmax_keys is not None and argmax_keys.numel() < ARGMAX_SLOTS * M:
+        raise NativeError(f"gemm: argmax_keys needs {ARGMAX_SLOTS} x M = {ARGMAX_SLOTS * M} entries")
+    if C is not None and C.dtype != A.dtype and C.dtype != torch.float32:
         raise NativeError("gemm: C must be f32 or the operand dtype")
-    out_f32 = 1 if C.dtype == torch.float32 else 0
+    out_f32 = 1 if C is not None and C.dtype == torch.float32 else 0
     if lda is None:
         lda = K if a_layout == K_CONTIG else M
     if ldb is None:
@@ -440,12 +444,13 @@ def gemm(A, B, C, M, N, K, *, a_layout=K_CONTIG, b_layout=K_CONTIG, lda=None, ld
                  ptr(residual), ldr if ldr is not None else ldc, ptr(aux), ld_aux if ld_aux is not None else ldc,
                  aux_scale, drop_p, ptr(seed), site, out_f32, 1 if accumulate else 0, ptr(rowsum), ptr(workspace),
                  0 if workspace is None else workspace.numel() * workspace.element_size(), ptr(ln_stats),
-                 ptr(ln_colsum), K // 64 if ln_stats is not None else 0, ln_eps, ptr(stats_out), tiles)
+                 ptr(ln_colsum), K // 64 if ln_stats is not None else 0, ln_eps, ptr(stats_out), tiles,
+                 ptr(argmax_keys))
     probe = _gemm_probe
     if probe is not None:
         # algorithmic bytes: operands once, output once (+ read-back of C / residual / aux when used)
         esz = A.element_size()
-        nbytes = (M * K + N * K) * esz + M * N * C.element_size() * (2 if accumulate else 1)
+        nbytes = (M * K + N * K) * esz + M * N * (C.element_size() if C is not None else 0) * (2 if accumulate else 1)
         nbytes += M * N * esz * ((residual is not None) + (aux is not None))
         probe.before(dt, a_layout, b_layout, M, N, K, nbytes)
     _check(lib().mit_gemm(ctypes.byref(g), stream_ptr()), "mit_gemm")

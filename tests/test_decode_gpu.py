@@ -373,7 +373,17 @@ def test_greedy_pick_advance_moves_pos_once():
     assert torch.equal(ids[:, 3], ids2[:, 3]) and torch.equal(ids[:, 4], ids2[:, 3])
 
 
-def test_decode_gemm_argmax_keys_exact():
+def _head_argmax(entry, a, w, bias, keys):
+    """The vocabulary head with the folded argmax through mit_decode_gemm or mit_gemm (the 128x128 kernel the
+    batched decode uses)."""
+    if entry == "decode_gemm":
+        N.decode_gemm(a, w, bias=bias, argmax_keys=keys)
+    else:
+        N.gemm(a, w, None, a.shape[0], w.shape[0], a.shape[1], bias=bias, argmax_keys=keys)
+
+
+@pytest.mark.parametrize("entry", ["decode_gemm", "gemm"])
+def test_decode_gemm_argmax_keys_exact(entry):
     """The greedy pick folded into the head GEMM (argmax_keys) against torch.argmax on exact arithmetic
     (small-integer bf16 operands: every partial sum is exact in f32, so any summation order gives the same
     logits and ties are real): first maximal column on ties, NaN largest; then mit_greedy_pick_keys writes
@@ -394,7 +404,7 @@ def test_decode_gemm_argmax_keys_exact():
         if case == 2:  # NaN columns are maximal; the first one wins
             bias[7] = bias[3000] = float("nan")
         bias = bias.to(dev)
-        N.decode_gemm(a, w, bias=bias, argmax_keys=keys)
+        _head_argmax(entry, a, w, bias, keys)
         want = (ref + bias.double()).argmax(1)
         got = N.argmax_of_keys(keys, M)
         assert torch.equal(got, want), (case, (got != want).sum().item())
@@ -413,8 +423,9 @@ def test_decode_gemm_argmax_keys_exact():
         assert nf.item() == int((want[1:] == end).sum()) and fin[1].item() == 1
 
 
+@pytest.mark.parametrize("entry", ["decode_gemm", "gemm"])
 @pytest.mark.parametrize("V", [509, 1001, 7])
-def test_decode_gemm_argmax_keys_ragged_vocab(V):
+def test_decode_gemm_argmax_keys_ragged_vocab(V, entry):
     """argmax_keys on a vocabulary that is not a multiple of 8 (padded_vocab's case): the head runs on the
     V real rows and no column >= V can win, even when the weight memory past row V holds larger values."""
     dev = torch.device("cuda")
@@ -427,7 +438,7 @@ def test_decode_gemm_argmax_keys_ragged_vocab(V):
     bias = torch.randint(-4, 5, (V + 8,), generator=g).float().to(dev)
     bias[V:] = 1e4
     keys = torch.zeros(N.ARGMAX_SLOTS * M, dtype=torch.int64, device=dev)
-    N.decode_gemm(a, w, bias=bias[:V], argmax_keys=keys)
+    _head_argmax(entry, a, w, bias[:V], keys)
     want = (a.double() @ w.double().t() + bias[:V].double()).argmax(1)
     got = N.argmax_of_keys(keys, M)
     assert torch.equal(got, want)
@@ -442,6 +453,10 @@ def test_decode_gemm_argmax_keys_rejects_outputs():
         N.decode_gemm(a, w, out=torch.empty(4, 64, device=dev, dtype=torch.bfloat16), argmax_keys=keys)
     with pytest.raises(N.NativeError, match="argmax_keys"):
         N.decode_gemm(a, w, act=N.ACT_RELU, argmax_keys=keys)
+    with pytest.raises(N.NativeError, match="argmax_keys"):
+        N.gemm(a, w, torch.empty(4, 64, device=dev, dtype=torch.bfloat16), 4, 64, 64, argmax_keys=keys)
+    with pytest.raises(N.NativeError, match="argmax_keys"):
+        N.gemm(a, w, None, 4, 64, 64, act=N.ACT_RELU, argmax_keys=keys)
 
 
 @pytest.mark.parametrize("name", ["tiny_vit_patches", "cfg0_b4_patches", "tiny_vit_v509"])
