@@ -148,10 +148,24 @@ __device__ __forceinline__ float quick_gelu(float x) {
 // -inf and NaN -> NaN (x * sigmoid(1.702 x) in torch: -inf * 0 = NaN). configs[2] 2028 -> 2048 pairs/s
 // (interleaved, one box); its parity side: profiles/r06_grad_metric_report.json (the trimmed worst-tensor
 // gradient metric moves 0.2-0.9 %). The scalar / fp32-parity path keeps the exact division (quick_gelu).
+// In pairs: the multiplies and the add as packed FP32 (v_pk_mul_f32 / v_pk_add_f32), the same roundings as
+// the scalar form (__expf(y) = v_exp_f32(y * log2(e))): bitwise identical, 4 packed VALU + 4 transcendentals
+// per two values instead of 8 + 4. (One multiply by the merged constant -1.702 log2(e) would save another,
+// but moves the exponent by an ulp on 29 % of inputs, and the fixtures' 64-pin worst-gradient metric with it.)
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 template <int N>
 __device__ __forceinline__ void quick_gelu_fast_n(float* v) {
+  static_assert(N % 2 == 0, "quick_gelu_fast_n: pairs of values");
+  constexpr float c = -1.702f, l2e = 1.44269504088896341f;
 #pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = v[k] * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[k]));
+  for (int k = 0; k < N; k += 2) {
+    const f32x2 x = {v[k], v[k + 1]};
+    const f32x2 z = (x * f32x2{c, c}) * f32x2{l2e, l2e};
+    const f32x2 d = f32x2{__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])} + f32x2{1.0f, 1.0f};
+    const f32x2 r = x * f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+    v[k] = r[0];
+    v[k + 1] = r[1];
+  }
 }
 // GELU (erf form) for bf16 epilogues with ONE transcendental and no select: x Phi(x) = max(x, 0) - a h,
 // a = min(|x|, 6), h = Phi(-a) = 2^q(a), q a degree-7 fit of log2 Phi(-a) on [0, 6] (tools/gelu_fit.py):
@@ -173,17 +187,16 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return fmaf(-a, __builtin_amdgcn_exp2f(p), fmaxf(x, 0.0f));
 }
 
-// gelu_fast on two values: the polynomial in packed FP32 (v_pk_fma_f32, two values per instruction);
-// min / exp2 / the final max + fma scalar
-typedef __attribute__((ext_vector_type(2))) float f32x2;
+// gelu_fast on two values: the polynomial and the final FMA in packed FP32 (v_pk_fma_f32, two values per
+// instruction); min / exp2 / max scalar
 __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
   constexpr float q[8] = {MIT_GELU_Q(MIT_GELU_S)};
   const f32x2 a = {__builtin_elementwise_minimum(fabsf(x[0]), 6.0f), __builtin_elementwise_minimum(fabsf(x[1]), 6.0f)};
   f32x2 p = __builtin_elementwise_fma(f32x2{q[0], q[0]}, a, f32x2{q[1], q[1]});
 #pragma unroll
   for (int k = 2; k < 8; ++k) p = __builtin_elementwise_fma(p, a, f32x2{q[k], q[k]});
-  return f32x2{fmaf(-a[0], __builtin_amdgcn_exp2f(p[0]), fmaxf(x[0], 0.0f)),
-               fmaf(-a[1], __builtin_amdgcn_exp2f(p[1]), fmaxf(x[1], 0.0f))};
+  const f32x2 h = {__builtin_amdgcn_exp2f(p[0]), __builtin_amdgcn_exp2f(p[1])};
+  return __builtin_elementwise_fma(-a, h, f32x2{fmaxf(x[0], 0.0f), fmaxf(x[1], 0.0f)});
 }
 #undef MIT_GELU_S
 #undef MIT_GELU_Q

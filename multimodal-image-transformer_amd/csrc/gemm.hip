@@ -797,9 +797,15 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float v[4];
-        if constexpr (LNX == 1) {
+        if constexpr (LNX == 1) {  // in pairs (v_pk_fma_f32: the same fused ops as two v_fma_f32)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) v[t] = fmaf(acc[i][j][t], rs_i[i], fmaf(nr_i[i], sj[j][t], bj[j][t]));
+          for (int t = 0; t < 4; t += 2) {
+            const f32x2 c = __builtin_elementwise_fma(f32x2{nr_i[i], nr_i[i]}, f32x2{sj[j][t], sj[j][t + 1]},
+                                                      f32x2{bj[j][t], bj[j][t + 1]});
+            const f32x2 r = __builtin_elementwise_fma(f32x2{acc[i][j][t], acc[i][j][t + 1]}, f32x2{rs_i[i], rs_i[i]}, c);
+            v[t] = r[0];
+            v[t + 1] = r[1];
+          }
         } else {
 #pragma unroll
           for (int t = 0; t < 4; ++t) v[t] = acc[i][j][t] * e.alpha + bj[j][t];

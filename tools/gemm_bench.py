@@ -15,6 +15,7 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("dW kv_all", 6144, 512, 12608, 1, 1), ("dX kv_all", 12608, 512, 6144, 0, 1), ("dW ffn1", 2048, 512, 4032, 1, 1),
     ("4096^3", 4096, 4096, 4096, 0, 0),
     ("enc fc1+gelu", 12608, 3072, 768, 0, 0, "gelu"), ("enc fc2+res", 12608, 768, 3072, 0, 0, "res"),
+    ("enc qkv+ln", 12608, 2304, 768, 0, 0, "lnbias"), ("enc fc1+gelu+ln", 12608, 3072, 768, 0, 0, "lngelu"),
     ("enc qkv+bias", 12608, 2304, 768, 0, 0, "bias"), ("enc o+res", 12608, 768, 768, 0, 0, "res"), ("dec ffn1+relu+drop", 4032, 2048, 512, 0, 0, "reludrop"),
     # the d_model = 512 decoder GEMMs (128 output tiles)
     ("fwd out+bias", 4032, 512, 512, 0, 0, "bias"), ("fwd lin2+res", 4032, 512, 2048, 0, 0, "res"),
@@ -53,8 +54,12 @@ def run(iters=20, variants=(1, 2)):
             kw["residual"] = torch.randn(M, N, device=dev).to(torch.bfloat16)
         elif epi:
             kw["bias"] = torch.randn(N, device=dev)
-        if epi == "gelu":
+        if epi in ("gelu", "lngelu"):
             kw["act"] = native.ACT_GELU
+        if epi.startswith("ln"):  # the LayerNorm-folded encoder GEMMs (qkv, fc1): (mean, M2) per 64 columns of A
+            mean = 0.1 * torch.randn(M, K // 64, device=dev)
+            m2 = 64.0 * (0.5 + torch.rand(M, K // 64, device=dev))
+            kw.update(ln_stats=torch.stack([mean, m2], -1).contiguous(), ln_colsum=torch.randn(N, device=dev), ln_eps=1e-5)
         if epi == "qgelu":
             kw["act"] = native.ACT_QUICK_GELU
         if epi == "res":
