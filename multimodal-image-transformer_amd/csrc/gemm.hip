@@ -826,10 +826,11 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
         const int ch = 2 * j + (g >> 1);
         char* seg = stg + rr * 128 + ((ch ^ (rr & 7)) << 4) + (g & 1) * 8;
         if constexpr (XOPS) {
+          // LNX 2 (mit_gemm checked it): a residual, no aux operand, no dropout -- no run-time selects
           const u32x2 x = *(const u32x2*)seg;
           const float x0 = __uint_as_float(x[0] << 16), x1 = __uint_as_float(x[0] & 0xFFFF0000u);
           const float x2 = __uint_as_float(x[1] << 16), x3 = __uint_as_float(x[1] & 0xFFFF0000u);
-          if (e.aux) {
+          if (LNX != 2 && e.aux) {
             v[0] *= x0 > 0.f ? e.aux_scale : 0.f;
             v[1] *= x1 > 0.f ? e.aux_scale : 0.f;
             v[2] *= x2 > 0.f ? e.aux_scale : 0.f;
@@ -840,7 +841,7 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
 #pragma unroll
             for (int t = 0; t < 4; ++t) v[t] *= drop_mul(key, base + t, e.thresh, e.dscale);
           }
-          if (e.res) {
+          if (LNX == 2 || e.res) {
             v[0] += x0;
             v[1] += x1;
             v[2] += x2;
@@ -854,12 +855,14 @@ __device__ __forceinline__ void stage_epilogue(const f32x4 (&acc)[8][4], const E
         typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
         const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         *(bf16x4*)seg = o;
-        if constexpr (LNX == 2) {
+        if constexpr (LNX == 2) {  // the rounded values from the packed words (one shift / mask each)
+          const u32x2 w = __builtin_bit_cast(u32x2, o);
+          vr[j][0] = __uint_as_float(w[0] << 16);
+          vr[j][1] = __uint_as_float(w[0] & 0xFFFF0000u);
+          vr[j][2] = __uint_as_float(w[1] << 16);
+          vr[j][3] = __uint_as_float(w[1] & 0xFFFF0000u);
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            vr[j][t] = (float)o[t];
-            st_s += vr[j][t];
-          }
+          for (int t = 0; t < 4; ++t) st_s += vr[j][t];
         }
       }
       if constexpr (LNX == 2) {  // (mean, M2) of the row's 64 columns nw .. nw + 63 (two passes)

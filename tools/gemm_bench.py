@@ -15,6 +15,7 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("dW kv_all", 6144, 512, 12608, 1, 1), ("dX kv_all", 12608, 512, 6144, 0, 1), ("dW ffn1", 2048, 512, 4032, 1, 1),
     ("4096^3", 4096, 4096, 4096, 0, 0),
     ("enc fc1+gelu", 12608, 3072, 768, 0, 0, "gelu"), ("enc fc2+res", 12608, 768, 3072, 0, 0, "res"),
+    ("enc o+res+st", 12608, 768, 768, 0, 0, "resst"), ("enc fc2+res+st", 12608, 768, 3072, 0, 0, "resst"),
     ("enc qkv+ln", 12608, 2304, 768, 0, 0, "lnbias"), ("enc fc1+gelu+ln", 12608, 3072, 768, 0, 0, "lngelu"),
     ("enc qkv+bias", 12608, 2304, 768, 0, 0, "bias"), ("enc o+res", 12608, 768, 768, 0, 0, "res"), ("dec ffn1+relu+drop", 4032, 2048, 512, 0, 0, "reludrop"),
     # the d_model = 512 decoder GEMMs (128 output tiles)
@@ -62,8 +63,10 @@ def run(iters=20, variants=(1, 2)):
             kw.update(ln_stats=torch.stack([mean, m2], -1).contiguous(), ln_colsum=torch.randn(N, device=dev), ln_eps=1e-5)
         if epi == "qgelu":
             kw["act"] = native.ACT_QUICK_GELU
-        if epi == "res":
+        if epi in ("res", "resst"):
             kw["residual"] = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        if epi == "resst":  # + the output rows' per-64-column (mean, M2): the folded encoder's o-proj / fc2
+            kw["stats_out"] = torch.empty(M, N // 64, 2, device=dev)
         if epi == "reludrop":
             kw.update(act=native.ACT_RELU, drop_p=0.1, seed=torch.tensor([7], device=dev), site=1)
         best = {}
