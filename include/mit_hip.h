@@ -133,8 +133,10 @@ int mit_gemm(const mit_gemm_args* args, void* stream);
 long mit_gemm_workspace_bytes(long M, long N, long K);
 /* Tile-kernel choice for bf16 GEMMs: 0 = per shape (default), 1 = 128x128 kernel only, 2 = 256x256
  * kernel wherever split-K is not planned, 3 = the 64x64 register-streaming kernel for every NT GEMM
- * without rowsum / split-K. Results are identical up to fp32 summation order; a test knob, not a
- * numerics switch. */
+ * without rowsum / split-K, 4 = as 0 with the one-wave-per-SIMD 256x256 kernel for the NT GEMMs it
+ * covers (K % 64 == 0; plain / bias / activation, LayerNorm fold, residual + statistics; bitwise equal to
+ * the 256x256 kernel). Results are identical up to fp32 summation order; a test knob, not a numerics
+ * switch. */
 int mit_gemm_set_variant(int variant);
 /* The launch mit_gemm would make for these args (no launch): returns the output tile edge of the
  * kernel (256 or 128 for bf16, 65 for the bf16 64x64 register-streaming kernel, 64 for the f32

@@ -32,6 +32,7 @@
 #include <stdlib.h>
 
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -1185,6 +1186,186 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
 }
 
 // ------------------------------------------------------------------------------------------------
+// 256x256 tile with ONE wave per SIMD (opt-in: mit_gemm_set_variant(4); NT, bf16, K % 64 == 0, the STG 1 /
+// 3 / 4 epilogues): 4 waves as 2 (M) x 2 (N), each owning a 128x128 output tile = 8 x 8 accumulator blocks
+// (256 registers per lane, AGPRs, accumulated in place by inline-asm MFMAs). The K-tile's LDS image and DMA
+// plan are gemm256_kernel's (each wave issues the pieces of two of its virtual waves; the K-tile step in
+// soffset). Per K-tile two phases of 64 MFMAs, one barrier:
+//   X(t): MFMAs of k-slice 0 of tile t  | ds_reads of k-slice 1 of tile t
+//   [own DMA of tile t+1 landed, own reads returned] barrier
+//   Y(t): DMA of tile t+2 into tile t's buffer, MFMAs of k-slice 1 | ds_reads of k-slice 0 of tile t+1
+// Every output element sums the same MFMAs in the same K order as gemm256_kernel: bitwise equal
+// (tests/test_gemm256_gpu.py). Measured (profiles/r06_gemm256w_ab.txt): one tile per CU on 8 CUs 10.6 vs
+// 18.3 us (K = 768), 4096^3 1350-1358 vs 1305-1315 TFLOP/s, but 4-12 % slower on the encoder's full-chip
+// shapes and the train step 2.3 % slower -- not the default.
+// ------------------------------------------------------------------------------------------------
+template <int ACT, int STG>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm256w_kernel(
+    const bf16* __restrict__ A, const bf16* __restrict__ B, void* C, long M, long N, long K, long lda, long ldb,
+    long ldc, int a_bytes, int b_bytes, Epi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  constexpr int BMT = 256;
+  const int nbn = (int)((N + B2 - 1) / B2), nbm = (int)((M + BMT - 1) / BMT);
+  const int ntiles = nbn * nbm;
+  const int bid = xcd_remap(blockIdx.x, ntiles);
+  const int GROUP = G256_GROUP;
+  const int group_id = bid / (GROUP * nbn);
+  const int first_m = group_id * GROUP;
+  const int gsize = min(nbm - first_m, GROUP);
+  const int bm = first_m + (bid % (GROUP * nbn)) % gsize;
+  const int bn = (bid % (GROUP * nbn)) / gsize;
+  const long m0 = (long)bm * BMT, n0 = (long)bn * B2;
+  MIT_DASSERT((int)blockIdx.x < ntiles && m0 < M && n0 < N);
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, b_bytes, 0x00020000);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)(K / BK);  // K % 64 == 0 (the dispatcher's condition)
+  // LDS-DMA sources: piece p = (operand X, half h, virtual wave vw = wid + 4 v, instruction j) of a K-tile;
+  // the voffset (row / k-chunk, OOB past the operand) is fixed, the K-tile's byte step goes in soffset
+  // (scalar), the LDS destination is wave-uniform (M0): scalar ops only per piece in the loop
+  uint32_t voff[2][2][2][2];  // [X][h][v][j]
+#pragma unroll
+  for (int X = 0; X < 2; ++X)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int id = ((wid + 4 * v) * 2 + j) * 64 + lane;
+        const int r = id >> 3, c = (id & 7) ^ ((r >> 1) & 7);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const long row = (X ? n0 : m0) + h * 128 + r;
+          const long ld = X ? ldb : lda;
+          voff[X][h][v][j] = row < (X ? N : M) ? (uint32_t)((row * ld + c * 8) * 2) : OOB;
+        }
+      }
+  // a tile t >= nk loads nothing (soffset past any num_records: the pieces read as zeros into a buffer no
+  // one reads again; the epilogue waits vmcnt(0) before reusing it), so every K-tile runs the same code
+  auto issue_piece = [&](int t, int p) {  // p = ((X * 2 + h) * 2 + v) * 2 + j
+    const int X = p >> 3, h = (p >> 2) & 1, v = (p >> 1) & 1, j = p & 1;
+    char* dst = smem + (t & 1) * BUF_BYTES + (X * 2 + h) * HALF_BYTES + (wid + 4 * v) * 2048 + j * 1024;
+    const int soff = t < nk ? t * BK * 2 : (int)OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(X ? rb : ra, (__attribute__((address_space(3))) void*)dst, 16,
+                                             voff[X][h][v][j], soff, 0, 0);
+  };
+  auto issue_tile = [&](int t) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) issue_piece(t, p);
+  };
+  bf16x8 fa[2][8], fb[2][8];
+  auto read_frag = [&](int t, int kk, int q) {  // q < 8: A row block q, else B column block q - 8
+    const char* buf = smem + (t & 1) * BUF_BYTES;
+    if (q < 8) fa[kk][q] = frag<MIT_K_CONTIG>(buf + wr * HALF_BYTES, q * 16, kk, lane);
+    else fb[kk][q - 8] = frag<MIT_K_CONTIG>(buf + (2 + wc) * HALF_BYTES, (q - 8) * 16, kk, lane);
+  };
+  // in-place accumulation (dst = srcC, "+a": the accumulators stay put in the AGPRs; with the builtin the
+  // register allocator re-homed some of the 64 blocks every K-tile, ~130 v_accvgpr copies per iteration)
+  auto mma4 = [&](int kk, int n) {  // MFMAs 4n .. 4n+3 of the k-slice (row block n / 2, four column blocks)
+    const int i = n >> 1;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = (n & 1) * 4 + jj;
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fb[kk][j]), "v"(fa[kk][i]));
+    }
+  };
+  // One fragment read and one DMA piece per group of four MFMAs. Measured on 4096^3 (tools/gemm_bench.py,
+  // profiles/r06_gemm256w_ab.txt): the DMA pieces cost ~14 % (issued among this wave's own MFMAs: no partner
+  // wave's MFMAs cover their issue), the fragment reads ~8 %, the barrier ~2.5 %; splitting the pieces over
+  // both phases (half a phase to land) measured the same.
+  // X(t): k-slice 0's 64 MFMAs | k-slice 1's reads of tile t
+  auto phase_x = [&](int t) {
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      read_frag(t, 1, n);
+      mma4(0, n);
+    }
+  };
+  // Y(t): k-slice 1's 64 MFMAs | the DMA of tile t+2, k-slice 0's reads of tile t+1 (past the last tile:
+  // stale contents into registers no MFMA uses)
+  auto phase_y = [&](int t) {
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      issue_piece(t + 2, n);
+      read_frag(t + 1, 0, n);
+      mma4(1, n);
+    }
+  };
+
+  // prologue: bias / LN-fold operands staged as gemm256_kernel does, K-tiles 0 and 1 in flight
+  f32x2* ln_rows = (f32x2*)(smem + SMEM2_BYTES);
+  float* lcol = (float*)(smem + SMEM2_BYTES + 2048);
+  float pbias = 0.f, pcols = 0.f;
+  {
+    const long c = n0 + tid;
+    if (c < N) {
+      if (e.bias) pbias = e.bias[c];
+      if constexpr (STG == 3) pcols = e.ln_colsum[c];
+    }
+  }
+  f32x2 lnp[STG == 3 ? LN_PMAX : 1];
+  if constexpr (STG == 3) {
+    const long row = m0 + tid;
+    const bool ok = row < M;
+#pragma unroll
+    for (int p = 0; p < LN_PMAX; ++p)
+      lnp[p] = (ok && p < e.ln_parts) ? *(const f32x2*)(e.ln_stats + (row * e.ln_parts + p) * 2) : f32x2{0.f, 0.f};
+  }
+  issue_tile(0);
+  issue_tile(1);
+  if constexpr (STG == 3) {
+    float mu = 0.f, q = 0.f;
+#pragma unroll
+    for (int p = 0; p < LN_PMAX; ++p)
+      if (p < e.ln_parts) {
+        const float d = lnp[p][0] - mu, f = 1.0f / (float)(p + 1);
+        mu = fmaf(d, f, mu);
+        q += lnp[p][1] + d * d * (64.0f * (float)p * f);
+      }
+    const float rs = __builtin_amdgcn_rsqf(q / (64.0f * (float)e.ln_parts) + e.ln_eps);
+    ln_rows[tid] = f32x2{rs, -rs * mu};
+  }
+  lcol[tid] = pbias;
+  if constexpr (STG == 3) lcol[256 + tid] = pcols;
+  asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+  bar_raw();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) read_frag(0, 0, q);
+
+  for (int t = 0; t < nk; ++t) {
+    phase_x(t);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // tile t+1 landed; k-slice 1 returned
+    bar_raw();                                                  // ... on every wave: tile t's buffer is free
+    phase_y(t);
+  }
+  // the last MFMAs' results reach the AGPRs before any VALU reads them (the hazard recognizer does not see
+  // into the asm): 3 x 8 wait states past the 16x16x32 MFMA's 8 passes
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  bar_raw();  // every wave's last reads returned: the K-tile buffers become the epilogue stages
+
+  char* stg = smem + wid * 16384;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32x4 a2[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a2[i][j] = acc[i][h * 4 + j];
+    stage_epilogue<ACT, false, STG == 4, STG == 3 ? 1 : (STG == 4 ? 2 : 0)>(
+        a2, e, C, ldc, M, N, m0 + wr * 128, n0 + wc * 128 + h * 64, lane, stg, lcol + wc * 128 + h * 64, ln_rows + wr * 128);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Register-streaming NT kernel for the decode step's B-row GEMMs (M = B <= 256, short K: the 128
 // kernel runs 2 x N/128 blocks through a K loop bound by per-K-step DMA issue / barrier / fragment
 // read latency). 64x64 output tile per 4-wave block; no operand staging: each wave loads
@@ -1499,7 +1680,10 @@ void launch_rs(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_bytes, h
 
 // 0 = pick per shape, 1 = always the 128x128 kernel, 2 = the 256x256 kernel wherever it has an
 // instance for the epilogue, 3 = the register-streaming kernel where it applies (tests / tools)
-int g_variant = 0;
+#ifndef MIT_GEMM_DEFAULT_VARIANT
+#define MIT_GEMM_DEFAULT_VARIANT 0  // A/B builds (tools/build_variants.sh) may start in another variant
+#endif
+int g_variant = MIT_GEMM_DEFAULT_VARIANT;
 int gemm_variant() { return g_variant; }
 
 // bf16 outputs with a gatherable epilogue leave through each wave's LDS stage (STG 1: no operand,
@@ -1521,6 +1705,31 @@ void launch_bf16_256(const mit_gemm_args* g, const Epi& e, int a_bytes, int b_by
     attr = true;
   }
   const dim3 grid((unsigned)(nbm * nbn));
+  if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG && !DROP) {  // one-wave-per-SIMD prototype (variant 4)
+    if (gemm_variant() == 4 && g->K % BK == 0 && (!e.res || e.stats_out) && !e.aux && !e.out_f32 && epi_gatherable(e)) {
+      static bool wattr = false;
+      if (!wattr) {
+        set_lds(gemm256w_kernel<ACT, 1>, SMEM2_EPI_BYTES);
+        set_lds(gemm256w_kernel<ACT, 3>, SMEM2_EPI_BYTES);
+        if constexpr (ACT == MIT_ACT_NONE) set_lds(gemm256w_kernel<ACT, 4>, SMEM2_EPI_BYTES);
+        wattr = true;
+      }
+      if constexpr (ACT == MIT_ACT_NONE) {
+        if (e.stats_out) {
+          hipLaunchKernelGGL((gemm256w_kernel<ACT, 4>), grid, dim3(256), SMEM2_EPI_BYTES, s, (const bf16*)g->A,
+                             (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
+          return;
+        }
+      }
+      if (e.ln_stats)
+        hipLaunchKernelGGL((gemm256w_kernel<ACT, 3>), grid, dim3(256), SMEM2_EPI_BYTES, s, (const bf16*)g->A,
+                           (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
+      else
+        hipLaunchKernelGGL((gemm256w_kernel<ACT, 1>), grid, dim3(256), SMEM2_EPI_BYTES, s, (const bf16*)g->A,
+                           (const bf16*)g->B, g->C, g->M, g->N, g->K, g->lda, g->ldb, g->ldc, a_bytes, b_bytes, e);
+      return;
+    }
+  }
   if constexpr (AL == MIT_K_CONTIG && BL == MIT_K_CONTIG) {  // LayerNorm fold / statistics (mit_gemm checked them)
     if constexpr (!DROP) {
       if (e.ln_stats) {
@@ -1572,7 +1781,7 @@ bool use_rs(const mit_gemm_args* g) {
   if (g->a_layout != MIT_K_CONTIG || g->b_layout != MIT_K_CONTIG || g->rowsum || g->ln_stats || g->stats_out) return false;
   const int v = gemm_variant();
   if (v == 3) return true;
-  if (v != 0) return false;
+  if (v != 0 && v != 4) return false;
   return g->M <= 256 && g->N <= 2048 && g->K <= 1024;
 }
 
@@ -1681,7 +1890,7 @@ Split plan_split(const mit_gemm_args* g) {
 }  // namespace
 
 extern "C" int mit_gemm_set_variant(int v) {
-  MIT_CHECK_ARG(v >= 0 && v <= 3, "mit_gemm_set_variant: %d not in {0,1,2,3}", v);
+  MIT_CHECK_ARG(v >= 0 && v <= 4, "mit_gemm_set_variant: %d not in {0,1,2,3,4}", v);
   g_variant = v;
   return MIT_OK;
 }

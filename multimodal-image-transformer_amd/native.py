@@ -520,7 +520,8 @@ def attention_set_index_limit(limit: float = 0.0):
 
 def gemm_set_variant(v):
     """0 = per-shape tile-kernel choice, 1 = 128x128 only, 2 = 256x256 wherever legal, 3 = 64x64
-    register-streaming kernel for NT GEMMs."""
+    register-streaming kernel for NT GEMMs, 4 = as 0 with the one-wave-per-SIMD 256x256 kernel for the NT
+    bf16 GEMMs it covers (gemm256w_kernel: bitwise equal, measured slower in the step)."""
     _check(lib().mit_gemm_set_variant(int(v)), "mit_gemm_set_variant")
 
 

@@ -324,3 +324,43 @@ def test_gemm_layernorm_fold_rejects_bad_args():
     st = torch.zeros(256, 4, 2, device=dev())
     with pytest.raises(N.NativeError, match="ln_stats"):  # K % 64 != 0
         N.gemm(x, w, out, 256, 256, 200, ln_stats=st, ln_colsum=torch.zeros(256, device=dev()))
+
+
+@pytest.mark.parametrize("M,Nn,K,kind", [(256, 256, 64, "plain"), (520, 776, 192, "bias"), (1000, 512, 256, "resst"),
+                                         (2056, 768, 768, "gelu"), (1032, 2304, 768, "lnbias"),
+                                         (1032, 3072, 768, "lngelu"), (300, 264, 1024, "qgelu")])
+def test_gemm256w_one_wave_per_simd_bitwise(M, Nn, K, kind):
+    """The opt-in one-wave-per-SIMD 256x256 kernel (mit_gemm_set_variant(4), gemm256w_kernel) sums the same
+    MFMAs in the same K order as gemm256_kernel: outputs (and STG 4 row statistics) bitwise equal, for the
+    plain / bias / GELU / quick_gelu / LayerNorm-folded / residual + statistics epilogues and ragged M / N."""
+    torch.manual_seed(3)
+    A = torch.randn(M, K, device=dev()).to(torch.bfloat16)
+    B = (0.05 * torch.randn(Nn, K, device=dev())).to(torch.bfloat16)
+    kw = {}
+    if kind != "plain":
+        kw["bias"] = torch.randn(Nn, device=dev())
+    if kind in ("gelu", "lngelu"):
+        kw["act"] = N.ACT_GELU
+    if kind == "qgelu":
+        kw["act"] = N.ACT_QUICK_GELU
+    if kind == "resst":
+        kw["residual"] = torch.randn(M, Nn, device=dev()).to(torch.bfloat16)
+    if kind.startswith("ln"):
+        mean = 0.1 * torch.randn(M, K // 64, device=dev())
+        m2 = 64.0 * (0.5 + torch.rand(M, K // 64, device=dev()))
+        kw.update(ln_stats=torch.stack([mean, m2], -1).contiguous(), ln_colsum=torch.randn(Nn, device=dev()), ln_eps=1e-5)
+    outs = []
+    for v in (0, 4):
+        N.gemm_set_variant(v)
+        C = torch.full((M, Nn), float("nan"), device=dev(), dtype=torch.bfloat16)
+        st = torch.full((M, Nn // 64, 2), float("nan"), device=dev()) if kind == "resst" else None
+        N.gemm(A, B, C, M, Nn, K, tiles=256, stats_out=st, **kw)
+        torch.cuda.synchronize()
+        outs.append((C, st))
+    N.gemm_set_variant(0)
+    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16))
+    if kind == "resst":
+        assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32))
+    ref = A.float() @ B.float().t()
+    if kind in ("plain",):
+        assert _rel(outs[1][0], ref) < 1e-2
