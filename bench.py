@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 FLOP/clk (MI355X_MICROARCH.md, dense)
-PMC_SUMMARIES = ("r06_pmc.json", "r05_pmc.json", "r04_pmc.json")  # the newest committed PMC summary is used
+PMC_SUMMARIES = ("r06f_pmc.json", "r06_pmc.json", "r05_pmc.json", "r04_pmc.json")  # the newest committed PMC summary is used
 METRIC = "image-caption pairs/sec (train step), 6L/d512 decoder + ViT-B/16, 1/2/4/8 GPU"
 
 
