@@ -1,5 +1,5 @@
 """Concurrency timeline of ONE train step from a rocprofv3 --kernel-trace CSV (eager bench run; the
-step = dispatches between the last two AdamW launches): wall, time with 0 / 1 / 2 / 3+ kernels in
+step = the end of one AdamW to the end of the next, every dispatch overlapping it, clipped): wall, time with 0 / 1 / 2 / 3+ kernels in
 flight, per-queue busy time, and per kernel family the time it ran ALONE (nothing else on the chip:
 the critical-path suspects). Usage: python tools/step_timeline.py kernel_trace.csv"""
 import collections
@@ -27,12 +27,16 @@ def main():
     spans = [(int(rows[j]["End_Timestamp"]) - int(rows[i + 1]["Start_Timestamp"]), i + 1, j + 1)
              for i, j in zip(ad, ad[1:]) if not any("spin" in r["Kernel_Name"] for r in rows[i + 1:j + 1])]
     _, a, b = min(spans)
-    step = rows[a:b]
-    t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
+    # the step: from the end of one AdamW to the end of the next, with EVERY dispatch that overlaps that
+    # interval (clipped to it) -- also the next step's kernels that start while the closing AdamW runs, which a
+    # window by dispatch order would drop (it made AdamW look alone)
+    t0, t1 = int(rows[a - 1]["End_Timestamp"]), int(rows[b - 1]["End_Timestamp"])
+    step = [r for r in rows if int(r["Start_Timestamp"]) < t1 and int(r["End_Timestamp"]) > t0
+            and "spin" not in r["Kernel_Name"]]
     ev = []
     for i, r in enumerate(step):
-        ev.append((int(r["Start_Timestamp"]), 1, i))
-        ev.append((int(r["End_Timestamp"]), -1, i))
+        ev.append((max(int(r["Start_Timestamp"]), t0), 1, i))
+        ev.append((min(int(r["End_Timestamp"]), t1), -1, i))
     ev.sort()
     active = set()
     hist = collections.Counter()
@@ -58,7 +62,7 @@ def main():
     if qkey:
         q = collections.Counter()
         for r in step:
-            q[r[qkey]] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            q[r[qkey]] += min(int(r["End_Timestamp"]), t1) - max(int(r["Start_Timestamp"]), t0)
         for k, v in sorted(q.items()):
             print(f"  {qkey} {k}: kernel time {v / 1e3:.1f} us")
     print("ran alone (us):")
