@@ -20,6 +20,7 @@ SHAPES = [  # name, M, N, K, a_layout, b_layout
     ("enc qkv+bias", 12608, 2304, 768, 0, 0, "bias"), ("enc o+res", 12608, 768, 768, 0, 0, "res"), ("dec ffn1+relu+drop", 4032, 2048, 512, 0, 0, "reludrop"),
     # the d_model = 512 decoder GEMMs (128 output tiles)
     ("fwd out+bias", 4032, 512, 512, 0, 0, "bias"), ("fwd lin2+res", 4032, 512, 2048, 0, 0, "res"),
+    ("fwd self_in+bias", 4032, 1536, 512, 0, 0, "bias"), ("fwd lin2+bias", 4032, 512, 2048, 0, 0, "bias"),
     ("dX out", 4032, 512, 512, 0, 1), ("dX q+res", 4032, 512, 512, 0, 1, "res0"),
     ("dX lin1+res", 4032, 512, 2048, 0, 1, "res0"), ("dX self_in+res", 4032, 512, 1536, 0, 1, "res0"),
     ("dX fc_out ws", 4032, 512, 10000, 0, 1, "ws"), ("dW dd ws", 512, 512, 4032, 1, 1, "ws"),
