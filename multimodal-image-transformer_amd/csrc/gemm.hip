@@ -1195,9 +1195,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16* __restrict__ A
 //   [own DMA of tile t+1 landed, own reads returned] barrier
 //   Y(t): DMA of tile t+2 into tile t's buffer, MFMAs of k-slice 1 | ds_reads of k-slice 0 of tile t+1
 // Every output element sums the same MFMAs in the same K order as gemm256_kernel: bitwise equal
-// (tests/test_gemm256_gpu.py). Measured (profiles/r06_gemm256w_ab.txt): one tile per CU on 8 CUs 10.6 vs
-// 18.3 us (K = 768), 4096^3 1350-1358 vs 1305-1315 TFLOP/s, but 4-12 % slower on the encoder's full-chip
-// shapes and the train step 2.3 % slower -- not the default.
+// (tests/test_gemm256_gpu.py). Measured (profiles/r06_gemm256w_ab.txt): 4096^3 1350-1358 vs 1305-1315 TFLOP/s,
+// but 4-12 % slower on the encoder's shapes and the train step 2.3 % slower -- not the default.
 // ------------------------------------------------------------------------------------------------
 template <int ACT, int STG>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm256w_kernel(
